@@ -1,0 +1,778 @@
+// TEST ORACLE ONLY -- CPU restatement of the Groth16 hot path of
+// ingonyama-zk/gnark-icicle (reference snapshot at /root/reference).
+//
+// Used by tests/ (as the parity checker), by the golden-fixture generator and by
+// bench.py's cpu_baseline leg.  It is never linked into, called by or shipped
+// with the product library (gnark-icicle_amd/).
+//
+// Restated reference behaviour (file:line in /root/reference):
+//   o_msm              G1Jac.MultiExp / G2Jac.MultiExp at backend/groth16/bn254/prove.go:204,217,
+//                      237,247,293 (gnark-crypto, not vendored): sum_i int(s_i) P_i with s_i a
+//                      Montgomery fr.Element and (0,0) = infinity.  Bucket (Pippenger) method.
+//   o_fft              fft.Domain.FFT / FFTInverse (prove.go:372-378,396): DIF natural->bitrev,
+//                      DIT bitrev->natural, OnCoset with FrMultiplicativeGen, FFTInverse scales 1/n.
+//   o_compute_h        computeH prove.go:356-399 (h returned bit-reversed).
+//   o_batch_mul_base   curve.BatchScalarMultiplicationG1/G2 (setup.go:251,320; prove.go:195).
+//   o_g16_setup        Setup setup.go:85-349 (no BSB22 commitments): Lagrange-at-tau (setupABC
+//                      :364-445), infinity filtering (:212-237), K for private wires (:143-196),
+//                      Z = t^i (t^n-1)/delta bit-reversed and truncated to n-1 (:199-210,:265-267).
+//   o_g16_prove        Prove prove.go:62-325 minus the BSB22 commitment side path (a11):
+//                      A/B compaction (:157-178), deltas (:195), Ar (:213-224), Bs1 (:200-211),
+//                      Krs (:227-280), Bs (:283-305).
+//   o_g16_check        The verification equation in the exponent (equivalent to verify.go:49-150's
+//                      pairing check for a setup whose toxic waste is known).
+//
+// Parity status: no MSM / NTT / H known-answer vectors exist in the reference
+//  -> "parity unpinned" at the gnark-crypto boundary.  This file is
+// cross-checked against the independent big-integer restatement oracle/pyref.py
+// and against the reference-pinned curve constants (tests/test_oracle.py).
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <thread>
+#include <vector>
+
+#include "o_arith.hpp"
+
+using namespace orc;
+
+const uint8_t* curve_gen(int id, int g2);
+
+namespace {
+
+using BnFp2 = Fe2<BnFp, -1>;
+using BlsFp2 = Fe2<BlsFp, -5>;
+
+template <class FR, class FP, class FP2, int NBITS, int TWO_ADICITY, uint64_t COSET_GEN,
+          int CURVE_ID>
+struct Curve {
+  using Fr = FR;
+  using Fp = FP;
+  using G1F = Fe<FP>;
+  using G2F = FP2;
+  static constexpr int nbits = NBITS;
+  static constexpr int two_adicity = TWO_ADICITY;
+  static constexpr uint64_t coset_gen = COSET_GEN;
+  static constexpr int id = CURVE_ID;
+};
+
+using BN = Curve<BnFr, BnFp, BnFp2, 254, 28, 5, 0>;
+using BLS = Curve<BlsFr, BlsFp, BlsFp2, 253, 47, 22, 1>;
+
+// ---------------------------------------------------------------------------
+// helpers
+// ---------------------------------------------------------------------------
+template <class D>
+inline Fe<D> load_fe(const uint8_t* p) {
+  Fe<D> r;
+  memcpy(r.v, p, sizeof(r.v));
+  return r;
+}
+template <class D>
+inline void store_fe(uint8_t* p, const Fe<D>& a) {
+  memcpy(p, a.v, sizeof(a.v));
+}
+template <class F>
+inline Aff<F> load_aff(const uint8_t* p) {
+  Aff<F> r;
+  memcpy(&r, p, sizeof(r));
+  return r;
+}
+template <class F>
+inline void store_aff(uint8_t* p, const Aff<F>& a) {
+  memcpy(p, &a, sizeof(a));
+}
+
+template <class FN>
+void parallel_for(size_t n, int nthreads, FN fn) {
+  if (nthreads <= 1 || n < 2) {
+    fn(0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  size_t chunk = (n + nthreads - 1) / nthreads;
+  for (int t = 0; t < nthreads; t++) {
+    size_t s = t * chunk, e = std::min(n, s + chunk);
+    if (s >= e) break;
+    th.emplace_back([=] { fn(s, e); });
+  }
+  for (auto& x : th) x.join();
+}
+
+// Montgomery batch normalisation Jacobian -> affine
+template <class F>
+void batch_to_aff(const Jac<F>* in, Aff<F>* out, size_t n) {
+  std::vector<F> acc(n);
+  F run = FTraits<F>::one();
+  for (size_t i = 0; i < n; i++) {
+    acc[i] = run;
+    if (!is_zero(in[i].z)) run = mul(run, in[i].z);
+  }
+  F inv_run = inv(run);
+  for (size_t i = n; i-- > 0;) {
+    if (is_zero(in[i].z)) {
+      out[i] = {FTraits<F>::zero(), FTraits<F>::zero()};
+      continue;
+    }
+    F zi = mul(inv_run, acc[i]);
+    inv_run = mul(inv_run, in[i].z);
+    F zi2 = sqr(zi);
+    out[i] = {mul(in[i].x, zi2), mul(in[i].y, mul(zi2, zi))};
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Pippenger MSM (unsigned c-bit windows, Jacobian buckets with mixed adds)
+// ---------------------------------------------------------------------------
+inline uint32_t get_window(const uint64_t* k, int bit, int c) {
+  int w = bit >> 6, o = bit & 63;
+  uint64_t v = k[w] >> o;
+  if (o + c > 64 && w + 1 < 4) v |= k[w + 1] << (64 - o);
+  return (uint32_t)(v & ((1ull << c) - 1));
+}
+
+template <class C, class F>
+Jac<F> msm_pippenger(const std::vector<std::array<uint64_t, 4>>& k, const Aff<F>* pts, size_t n,
+                     int nthreads) {
+  if (n == 0) return jac_inf<F>();
+  int lg = 0;
+  while ((1ull << (lg + 1)) <= n) lg++;
+  int c = std::max(2, std::min(16, lg - 2));
+  int W = (C::nbits + c - 1) / c;
+  int nchunks = std::max(1, (2 * nthreads + W - 1) / W);
+  if ((size_t)nchunks > n) nchunks = (int)n;
+  size_t chunk = (n + nchunks - 1) / nchunks;
+  std::vector<Jac<F>> partial((size_t)W * nchunks, jac_inf<F>());
+  std::atomic<int> next(0);
+  auto worker = [&]() {
+    std::vector<Jac<F>> buckets((size_t)1 << c);
+    for (;;) {
+      int task = next.fetch_add(1);
+      if (task >= W * nchunks) break;
+      int w = task / nchunks, ch = task % nchunks;
+      size_t s = ch * chunk, e = std::min(n, s + chunk);
+      std::fill(buckets.begin(), buckets.end(), jac_inf<F>());
+      for (size_t i = s; i < e; i++) {
+        uint32_t d = get_window(k[i].data(), w * c, std::min(c, 256 - w * c));
+        if (d) buckets[d] = jadd_mixed(buckets[d], pts[i]);
+      }
+      Jac<F> run = jac_inf<F>(), tot = jac_inf<F>();
+      for (size_t d = buckets.size() - 1; d >= 1; d--) {
+        run = jadd(run, buckets[d]);
+        tot = jadd(tot, run);
+      }
+      partial[(size_t)w * nchunks + ch] = tot;
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 0; t < std::max(1, nthreads); t++) th.emplace_back(worker);
+  for (auto& x : th) x.join();
+  Jac<F> acc = jac_inf<F>();
+  for (int w = W - 1; w >= 0; w--) {
+    for (int i = 0; i < c; i++) acc = jdbl(acc);
+    for (int ch = 0; ch < nchunks; ch++) acc = jadd(acc, partial[(size_t)w * nchunks + ch]);
+  }
+  return acc;
+}
+
+template <class C>
+std::vector<std::array<uint64_t, 4>> canon_scalars(const uint8_t* scalars, size_t n, int nthreads) {
+  using Fr = typename C::Fr;
+  std::vector<std::array<uint64_t, 4>> k(n);
+  parallel_for(n, nthreads, [&](size_t s, size_t e) {
+    for (size_t i = s; i < e; i++) {
+      Fe<Fr> x = from_mont(load_fe<Fr>(scalars + 32 * i));
+      memcpy(k[i].data(), x.v, 32);
+    }
+  });
+  return k;
+}
+
+template <class C, class F>
+int msm_impl(const uint8_t* scalars, const uint8_t* points, size_t n, int nthreads, int naive,
+             uint8_t* out) {
+  auto k = canon_scalars<C>(scalars, n, nthreads);
+  const Aff<F>* pts = reinterpret_cast<const Aff<F>*>(points);
+  Jac<F> r;
+  if (naive) {
+    r = jac_inf<F>();
+    for (size_t i = 0; i < n; i++) r = jadd(r, scalar_mul(to_jac(pts[i]), k[i].data(), 4));
+  } else {
+    r = msm_pippenger<C, F>(k, pts, n, nthreads);
+  }
+  store_aff(out, to_aff(r));
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// FFT with gnark-crypto fft.Domain semantics
+// ---------------------------------------------------------------------------
+template <class C>
+Fe<typename C::Fr> domain_generator(int logn) {
+  using Fr = typename C::Fr;
+  // omega_n = omega_max^(2^(two_adicity - logn)); omega_max = g^((r-1)/2^s), g = coset_gen
+  // (pyref.py pins omega_max; here it is recomputed from the generator)
+  Fe<Fr> g = from_u64<Fr>(C::coset_gen);
+  uint64_t e[4];
+  for (int i = 0; i < 4; i++) e[i] = Fr::P[i];
+  e[0] -= 1;  // r - 1
+  // (r-1) >> two_adicity
+  int s = C::two_adicity;
+  // shift right by s bits
+  uint64_t q[4] = {0, 0, 0, 0};
+  for (int i = 0; i < 4; i++) {
+    int src = i + s / 64, off = s % 64;
+    uint64_t lo = src < 4 ? e[src] >> off : 0;
+    uint64_t hi = (off && src + 1 < 4) ? e[src + 1] << (64 - off) : 0;
+    q[i] = lo | hi;
+  }
+  Fe<Fr> w = pow(g, q, 4);
+  for (int i = 0; i < C::two_adicity - logn; i++) w = sqr(w);
+  return w;
+}
+
+inline size_t bitrev(size_t i, int logn) {
+  size_t r = 0;
+  for (int b = 0; b < logn; b++) r |= ((i >> b) & 1) << (logn - 1 - b);
+  return r;
+}
+
+template <class D>
+void fft_core(Fe<D>* a, size_t n, const Fe<D>& w, bool dit, int nthreads) {
+  // twiddles w^i, i < n/2
+  std::vector<Fe<D>> tw(std::max<size_t>(1, n / 2));
+  tw[0] = one<D>();
+  for (size_t i = 1; i < n / 2; i++) tw[i] = mul(tw[i - 1], w);
+  auto stage = [&](size_t m) {
+    size_t step = n / (2 * m);
+    size_t nb = n / 2;
+    auto body = [&](size_t s, size_t e) {
+      for (size_t t = s; t < e; t++) {
+        size_t blk = t / m, j = t % m;
+        size_t i0 = blk * 2 * m + j, i1 = i0 + m;
+        if (!dit) {
+          Fe<D> u = a[i0], v = a[i1];
+          a[i0] = add(u, v);
+          a[i1] = mul(sub(u, v), tw[j * step]);
+        } else {
+          Fe<D> u = a[i0], v = mul(a[i1], tw[j * step]);
+          a[i0] = add(u, v);
+          a[i1] = sub(u, v);
+        }
+      }
+    };
+    if (n >= (1u << 15)) parallel_for(nb, nthreads, body);
+    else body(0, nb);
+  };
+  if (!dit)
+    for (size_t m = n / 2; m >= 1; m /= 2) stage(m);
+  else
+    for (size_t m = 1; m < n; m *= 2) stage(m);
+}
+
+template <class C>
+int fft_impl(uint8_t* data, size_t n, int inverse, int dit, int coset, int nthreads) {
+  using Fr = typename C::Fr;
+  int logn = 0;
+  while ((1ull << logn) < n) logn++;
+  if ((1ull << logn) != n || logn > C::two_adicity) return -1;
+  Fe<Fr>* a = reinterpret_cast<Fe<Fr>*>(data);
+  Fe<Fr> w = domain_generator<C>(logn);
+  Fe<Fr> g = from_u64<Fr>(C::coset_gen);
+  if (!inverse) {
+    if (coset) {
+      parallel_for(n, nthreads, [&](size_t s, size_t e) {
+        for (size_t i = s; i < e; i++) {
+          size_t j = dit ? bitrev(i, logn) : i;
+          uint64_t ej[1] = {j};
+          a[i] = mul(a[i], pow(g, ej, 1));
+        }
+      });
+    }
+    fft_core(a, n, w, dit != 0, nthreads);
+  } else {
+    fft_core(a, n, inv(w), dit != 0, nthreads);
+    Fe<Fr> ninv = inv(from_u64<Fr>(n));
+    Fe<Fr> ginv = inv(g);
+    parallel_for(n, nthreads, [&](size_t s, size_t e) {
+      for (size_t i = s; i < e; i++) {
+        Fe<Fr> f = ninv;
+        if (coset) {
+          size_t j = dit ? i : bitrev(i, logn);
+          uint64_t ej[1] = {j};
+          f = mul(f, pow(ginv, ej, 1));
+        }
+        a[i] = mul(a[i], f);
+      }
+    });
+  }
+  return 0;
+}
+
+template <class C>
+int compute_h_impl(const uint8_t* a_in, const uint8_t* b_in, const uint8_t* c_in, size_t len,
+                   size_t n, int nthreads, uint8_t* h_out) {
+  using Fr = typename C::Fr;
+  if (len > n) return -1;
+  std::vector<Fe<Fr>> a(n, zero<Fr>()), b(n, zero<Fr>()), c(n, zero<Fr>());
+  memcpy(a.data(), a_in, 32 * len);
+  memcpy(b.data(), b_in, 32 * len);
+  memcpy(c.data(), c_in, 32 * len);
+  for (auto* v : {&a, &b, &c}) {
+    if (fft_impl<C>((uint8_t*)v->data(), n, 1, 0, 0, nthreads)) return -1;  // FFTInverse DIF
+    fft_impl<C>((uint8_t*)v->data(), n, 0, 1, 1, nthreads);                 // FFT DIT OnCoset
+  }
+  int logn = 0;
+  while ((1ull << logn) < n) logn++;
+  Fe<Fr> g = from_u64<Fr>(C::coset_gen);
+  uint64_t en[1] = {n};
+  Fe<Fr> den = inv(sub(pow(g, en, 1), one<Fr>()));
+  for (size_t i = 0; i < n; i++) a[i] = mul(sub(mul(a[i], b[i]), c[i]), den);
+  fft_impl<C>((uint8_t*)a.data(), n, 1, 0, 1, nthreads);  // FFTInverse DIF OnCoset
+  memcpy(h_out, a.data(), 32 * n);
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// fixed-base batch scalar multiplication (8-bit windowed table)
+// ---------------------------------------------------------------------------
+template <class C, class F>
+void batch_mul_base(const Aff<F>& base, const uint8_t* scalars_mont, size_t n, int nthreads,
+                    Aff<F>* out) {
+  const int c = 8, W = 32;
+  std::vector<Aff<F>> table((size_t)W * 256);
+  {
+    std::vector<Jac<F>> tj((size_t)W * 256);
+    Jac<F> b = to_jac(base);
+    for (int w = 0; w < W; w++) {
+      tj[(size_t)w * 256] = jac_inf<F>();
+      for (int d = 1; d < 256; d++) tj[(size_t)w * 256 + d] = jadd(tj[(size_t)w * 256 + d - 1], b);
+      for (int i = 0; i < c; i++) b = jdbl(b);
+    }
+    batch_to_aff(tj.data(), table.data(), tj.size());
+  }
+  parallel_for(n, nthreads, [&](size_t s, size_t e) {
+    std::vector<Jac<F>> tmp(e - s);
+    for (size_t i = s; i < e; i++) {
+      Fe<typename C::Fr> k = from_mont(load_fe<typename C::Fr>(scalars_mont + 32 * i));
+      Jac<F> r = jac_inf<F>();
+      for (int w = 0; w < W; w++) {
+        uint32_t d = (uint32_t)((k.v[w / 8] >> (8 * (w % 8))) & 0xff);
+        if (d) r = jadd_mixed(r, table[(size_t)w * 256 + d]);
+      }
+      tmp[i - s] = r;
+    }
+    batch_to_aff(tmp.data(), out + s, e - s);
+  });
+}
+
+// ---------------------------------------------------------------------------
+// Groth16 (no BSB22 commitments)
+// R1CS test format: CSR per matrix (L, R, O): rowptr[nc+1], wire[nnz] (u32), coeff[nnz] (Fr mont)
+// ---------------------------------------------------------------------------
+struct R1csView {
+  size_t nc, nb_wires, nb_public;
+  const uint32_t* rp[3];
+  const uint32_t* wire[3];
+  const uint8_t* coeff[3];
+};
+
+template <class C>
+struct Toxic {
+  Fe<typename C::Fr> t, alpha, beta, gamma, delta;
+};
+
+// A_i(t), B_i(t), C_i(t) -- setupABC setup.go:364-445
+template <class C>
+void setup_abc(const R1csView& r, size_t n, const Fe<typename C::Fr>& t,
+               std::vector<Fe<typename C::Fr>> abc[3]) {
+  using Fr = typename C::Fr;
+  int logn = 0;
+  while ((1ull << logn) < n) logn++;
+  Fe<Fr> w = domain_generator<C>(logn);
+  for (int m = 0; m < 3; m++) abc[m].assign(r.nb_wires, zero<Fr>());
+  // L_j(t) = w^j (t^n - 1) / (n (t - w^j))
+  uint64_t en[1] = {n};
+  Fe<Fr> tn1 = sub(pow(t, en, 1), one<Fr>());
+  Fe<Fr> ninv = inv(from_u64<Fr>(n));
+  Fe<Fr> wj = one<Fr>();
+  for (size_t j = 0; j < r.nc; j++) {
+    Fe<Fr> L = mul(mul(mul(wj, tn1), ninv), inv(sub(t, wj)));
+    for (int m = 0; m < 3; m++)
+      for (uint32_t q = r.rp[m][j]; q < r.rp[m][j + 1]; q++) {
+        uint32_t wi = r.wire[m][q];
+        Fe<Fr> co = load_fe<Fr>(r.coeff[m] + 32 * q);
+        abc[m][wi] = add(abc[m][wi], mul(co, L));
+      }
+    wj = mul(wj, w);
+  }
+}
+
+template <class C>
+struct PkView {
+  // sizes
+  size_t n, nb_wires, nbA, nbB, nbK;
+  uint8_t *g1_alpha, *g1_beta, *g1_delta, *g1_A, *g1_B, *g1_Z, *g1_K;
+  uint8_t *g2_beta, *g2_delta, *g2_B;
+  uint8_t *infA, *infB;
+};
+
+template <class C>
+int g16_setup(const R1csView& r, const Toxic<C>& tw, PkView<C>& pk, int nthreads) {
+  using Fr = typename C::Fr;
+  using G1F = typename C::G1F;
+  using G2F = typename C::G2F;
+  size_t n = 1;
+  while (n < r.nc) n <<= 1;
+  if (n != pk.n) return -1;
+  std::vector<Fe<Fr>> abc[3];
+  setup_abc<C>(r, n, tw.t, abc);
+  Fe<Fr> deltaInv = inv(tw.delta);
+  // K scalars for private wires (no commitments): (beta A + alpha B + C) / delta
+  std::vector<Fe<Fr>> pkK;
+  for (size_t i = r.nb_public; i < r.nb_wires; i++) {
+    Fe<Fr> v = add(add(mul(abc[0][i], tw.beta), mul(abc[1][i], tw.alpha)), abc[2][i]);
+    pkK.push_back(mul(v, deltaInv));
+  }
+  // Z scalars t^i (t^n - 1) / delta, i < n
+  std::vector<Fe<Fr>> Z(n);
+  uint64_t en[1] = {n};
+  Fe<Fr> zdt = mul(sub(pow(tw.t, en, 1), one<Fr>()), deltaInv);
+  for (size_t i = 0; i < n; i++) {
+    Z[i] = zdt;
+    zdt = mul(zdt, tw.t);
+  }
+  // infinity filtering
+  std::vector<Fe<Fr>> A, B;
+  for (size_t i = 0; i < r.nb_wires; i++) {
+    pk.infA[i] = is_zero(abc[0][i]);
+    pk.infB[i] = is_zero(abc[1][i]);
+    if (!pk.infA[i]) A.push_back(abc[0][i]);
+    if (!pk.infB[i]) B.push_back(abc[1][i]);
+  }
+  if (A.size() != pk.nbA || B.size() != pk.nbB || pkK.size() != pk.nbK) return -2;
+  // G1 points
+  std::vector<Fe<Fr>> g1s;
+  g1s.push_back(tw.alpha);
+  g1s.push_back(tw.beta);
+  g1s.push_back(tw.delta);
+  g1s.insert(g1s.end(), A.begin(), A.end());
+  g1s.insert(g1s.end(), B.begin(), B.end());
+  g1s.insert(g1s.end(), Z.begin(), Z.end());
+  g1s.insert(g1s.end(), pkK.begin(), pkK.end());
+  Aff<G1F> g1gen;
+  Aff<G2F> g2gen;
+  memcpy(&g1gen, curve_gen(C::id, 0), sizeof(g1gen));
+  memcpy(&g2gen, curve_gen(C::id, 1), sizeof(g2gen));
+  std::vector<Aff<G1F>> g1p(g1s.size());
+  batch_mul_base<C, G1F>(g1gen, (const uint8_t*)g1s.data(), g1s.size(), nthreads, g1p.data());
+  size_t off = 0;
+  store_aff(pk.g1_alpha, g1p[off++]);
+  store_aff(pk.g1_beta, g1p[off++]);
+  store_aff(pk.g1_delta, g1p[off++]);
+  memcpy(pk.g1_A, &g1p[off], sizeof(Aff<G1F>) * A.size());
+  off += A.size();
+  memcpy(pk.g1_B, &g1p[off], sizeof(Aff<G1F>) * B.size());
+  off += B.size();
+  // bitReverse full n points then keep n-1 (setup.go:265-267)
+  {
+    int logn = 0;
+    while ((1ull << logn) < n) logn++;
+    std::vector<Aff<G1F>> z(g1p.begin() + off, g1p.begin() + off + n);
+    for (size_t i = 0; i + 1 < n; i++) store_aff(pk.g1_Z + sizeof(Aff<G1F>) * i, z[bitrev(i, logn)]);
+  }
+  off += n;
+  memcpy(pk.g1_K, &g1p[off], sizeof(Aff<G1F>) * pkK.size());
+  // G2: B, beta, delta
+  std::vector<Fe<Fr>> g2s(B);
+  g2s.push_back(tw.beta);
+  g2s.push_back(tw.delta);
+  std::vector<Aff<G2F>> g2p(g2s.size());
+  batch_mul_base<C, G2F>(g2gen, (const uint8_t*)g2s.data(), g2s.size(), nthreads, g2p.data());
+  memcpy(pk.g2_B, g2p.data(), sizeof(Aff<G2F>) * B.size());
+  store_aff(pk.g2_beta, g2p[B.size()]);
+  store_aff(pk.g2_delta, g2p[B.size() + 1]);
+  return 0;
+}
+
+template <class C>
+int g16_prove(const PkView<C>& pk, size_t nb_public, const uint8_t* wires, const uint8_t* a,
+              const uint8_t* b, const uint8_t* c, size_t nc, const uint8_t* r_mont,
+              const uint8_t* s_mont, int nthreads, uint8_t* ar_out, uint8_t* bs_out,
+              uint8_t* krs_out) {
+  using Fr = typename C::Fr;
+  using G1F = typename C::G1F;
+  using G2F = typename C::G2F;
+  const size_t n = pk.n;
+  // H
+  std::vector<uint8_t> h(32 * n);
+  if (compute_h_impl<C>(a, b, c, nc, n, nthreads, h.data())) return -1;
+  // wire compaction (prove.go:157-178)
+  std::vector<uint8_t> wA, wB;
+  for (size_t i = 0; i < pk.nb_wires; i++) {
+    if (!pk.infA[i]) wA.insert(wA.end(), wires + 32 * i, wires + 32 * i + 32);
+    if (!pk.infB[i]) wB.insert(wB.end(), wires + 32 * i, wires + 32 * i + 32);
+  }
+  if (wA.size() != 32 * pk.nbA || wB.size() != 32 * pk.nbB) return -2;
+  Fe<Fr> r = load_fe<Fr>(r_mont), s = load_fe<Fr>(s_mont);
+  Fe<Fr> kr = neg(mul(r, s));
+  Fe<Fr> rc = from_mont(r), sc = from_mont(s), krc = from_mont(kr);
+  Jac<G1F> delta = to_jac(load_aff<G1F>(pk.g1_delta));
+  Jac<G1F> d0 = scalar_mul(delta, rc.v, 4), d1 = scalar_mul(delta, sc.v, 4),
+           d2 = scalar_mul(delta, krc.v, 4);
+  auto msm1 = [&](const uint8_t* sc_, const uint8_t* pts, size_t m) {
+    auto k = canon_scalars<C>(sc_, m, nthreads);
+    return msm_pippenger<C, G1F>(k, reinterpret_cast<const Aff<G1F>*>(pts), m, nthreads);
+  };
+  // Ar = sum A + alpha + r delta
+  Jac<G1F> ar = msm1(wA.data(), pk.g1_A, pk.nbA);
+  ar = jadd_mixed(ar, load_aff<G1F>(pk.g1_alpha));
+  ar = jadd(ar, d0);
+  // Bs1 = sum B + beta + s delta
+  Jac<G1F> bs1 = msm1(wB.data(), pk.g1_B, pk.nbB);
+  bs1 = jadd_mixed(bs1, load_aff<G1F>(pk.g1_beta));
+  bs1 = jadd(bs1, d1);
+  // Krs = sum K (private wires) + sum Z h[:n-1] + kr delta + s Ar + r Bs1
+  Jac<G1F> krs = msm1(wires + 32 * nb_public, pk.g1_K, pk.nbK);
+  Jac<G1F> krs2 = msm1(h.data(), pk.g1_Z, n - 1);
+  krs = jadd(krs, d2);
+  krs = jadd(krs, krs2);
+  krs = jadd(krs, scalar_mul(ar, sc.v, 4));
+  krs = jadd(krs, scalar_mul(bs1, rc.v, 4));
+  // Bs (G2) = sum B2 + s delta2 + beta2
+  auto k2 = canon_scalars<C>(wB.data(), pk.nbB, nthreads);
+  Jac<G2F> bs = msm_pippenger<C, G2F>(k2, reinterpret_cast<const Aff<G2F>*>(pk.g2_B), pk.nbB,
+                                      nthreads);
+  bs = jadd(bs, scalar_mul(to_jac(load_aff<G2F>(pk.g2_delta)), sc.v, 4));
+  bs = jadd_mixed(bs, load_aff<G2F>(pk.g2_beta));
+  store_aff(ar_out, to_aff(ar));
+  store_aff(krs_out, to_aff(krs));
+  store_aff(bs_out, to_aff(bs));
+  return 0;
+}
+
+// exponent-level verification for a known toxic waste
+template <class C>
+int g16_check(const R1csView& rv, const Toxic<C>& tw, const uint8_t* wires, const uint8_t* r_mont,
+              const uint8_t* s_mont, const uint8_t* ar, const uint8_t* bs, const uint8_t* krs) {
+  using Fr = typename C::Fr;
+  using G1F = typename C::G1F;
+  using G2F = typename C::G2F;
+  size_t n = 1;
+  while (n < rv.nc) n <<= 1;
+  std::vector<Fe<Fr>> abc[3];
+  setup_abc<C>(rv, n, tw.t, abc);
+  Fe<Fr> r = load_fe<Fr>(r_mont), s = load_fe<Fr>(s_mont);
+  Fe<Fr> sa = zero<Fr>(), sb = zero<Fr>(), spub = zero<Fr>();
+  for (size_t i = 0; i < rv.nb_wires; i++) {
+    Fe<Fr> w = load_fe<Fr>(wires + 32 * i);
+    sa = add(sa, mul(w, abc[0][i]));
+    sb = add(sb, mul(w, abc[1][i]));
+    if (i < rv.nb_public) {
+      Fe<Fr> k = add(add(mul(tw.beta, abc[0][i]), mul(tw.alpha, abc[1][i])), abc[2][i]);
+      spub = add(spub, mul(w, k));
+    }
+  }
+  Fe<Fr> ea = add(add(tw.alpha, sa), mul(r, tw.delta));
+  Fe<Fr> eb = add(add(tw.beta, sb), mul(s, tw.delta));
+  // a*b = alpha*beta + pub + c*delta
+  Fe<Fr> ec = mul(sub(sub(mul(ea, eb), mul(tw.alpha, tw.beta)), spub), inv(tw.delta));
+  Aff<G1F> g1;
+  Aff<G2F> g2;
+  memcpy(&g1, curve_gen(C::id, 0), sizeof(g1));
+  memcpy(&g2, curve_gen(C::id, 1), sizeof(g2));
+  Fe<Fr> eac = from_mont(ea), ebc = from_mont(eb), ecc = from_mont(ec);
+  Aff<G1F> xa = to_aff(scalar_mul(to_jac(g1), eac.v, 4));
+  Aff<G2F> xb = to_aff(scalar_mul(to_jac(g2), ebc.v, 4));
+  Aff<G1F> xc = to_aff(scalar_mul(to_jac(g1), ecc.v, 4));
+  int ok = 0;
+  if (memcmp(&xa, ar, sizeof(xa)) == 0) ok |= 1;
+  if (memcmp(&xb, bs, sizeof(xb)) == 0) ok |= 2;
+  if (memcmp(&xc, krs, sizeof(xc)) == 0) ok |= 4;
+  return ok;  // 7 = valid proof
+}
+
+}  // namespace
+
+// generator points in gnark layout (tools/gen_field_constants.py)
+static const uint64_t G_BN_G1[] = O_BN254_G1_GEN;
+static const uint64_t G_BN_G2[] = O_BN254_G2_GEN;
+static const uint64_t G_BLS_G1[] = O_BLS12377_G1_GEN;
+static const uint64_t G_BLS_G2[] = O_BLS12377_G2_GEN;
+const uint8_t* curve_gen(int id, int g2) {
+  if (id == 0) return (const uint8_t*)(g2 ? G_BN_G2 : G_BN_G1);
+  return (const uint8_t*)(g2 ? G_BLS_G2 : G_BLS_G1);
+}
+
+// ===========================================================================
+// C ABI for ctypes (tests / fixture generator / bench cpu_baseline)
+// ===========================================================================
+extern "C" {
+
+int o_msm(int curve, int g2, const uint8_t* scalars, const uint8_t* points, size_t n,
+          int nthreads, int naive, uint8_t* out_affine) {
+  if (curve == 0)
+    return g2 ? msm_impl<BN, BnFp2>(scalars, points, n, nthreads, naive, out_affine)
+              : msm_impl<BN, Fe<BnFp>>(scalars, points, n, nthreads, naive, out_affine);
+  if (curve == 1)
+    return g2 ? msm_impl<BLS, BlsFp2>(scalars, points, n, nthreads, naive, out_affine)
+              : msm_impl<BLS, Fe<BlsFp>>(scalars, points, n, nthreads, naive, out_affine);
+  return -1;
+}
+
+int o_fft(int curve, uint8_t* data, size_t n, int inverse, int dit, int coset, int nthreads) {
+  if (curve == 0) return fft_impl<BN>(data, n, inverse, dit, coset, nthreads);
+  if (curve == 1) return fft_impl<BLS>(data, n, inverse, dit, coset, nthreads);
+  return -1;
+}
+
+int o_compute_h(int curve, const uint8_t* a, const uint8_t* b, const uint8_t* c, size_t len,
+                size_t n, int nthreads, uint8_t* h_out) {
+  if (curve == 0) return compute_h_impl<BN>(a, b, c, len, n, nthreads, h_out);
+  if (curve == 1) return compute_h_impl<BLS>(a, b, c, len, n, nthreads, h_out);
+  return -1;
+}
+
+int o_batch_mul_base(int curve, int g2, const uint8_t* base, const uint8_t* scalars, size_t n,
+                     int nthreads, uint8_t* out) {
+  if (curve == 0) {
+    if (g2) {
+      Aff<BnFp2> b;
+      memcpy(&b, base, sizeof(b));
+      batch_mul_base<BN, BnFp2>(b, scalars, n, nthreads, reinterpret_cast<Aff<BnFp2>*>(out));
+    } else {
+      Aff<Fe<BnFp>> b;
+      memcpy(&b, base, sizeof(b));
+      batch_mul_base<BN, Fe<BnFp>>(b, scalars, n, nthreads, reinterpret_cast<Aff<Fe<BnFp>>*>(out));
+    }
+    return 0;
+  }
+  if (curve == 1) {
+    if (g2) {
+      Aff<BlsFp2> b;
+      memcpy(&b, base, sizeof(b));
+      batch_mul_base<BLS, BlsFp2>(b, scalars, n, nthreads, reinterpret_cast<Aff<BlsFp2>*>(out));
+    } else {
+      Aff<Fe<BlsFp>> b;
+      memcpy(&b, base, sizeof(b));
+      batch_mul_base<BLS, Fe<BlsFp>>(b, scalars, n, nthreads,
+                                     reinterpret_cast<Aff<Fe<BlsFp>>*>(out));
+    }
+    return 0;
+  }
+  return -1;
+}
+
+const uint8_t* o_generator(int curve, int g2) { return curve_gen(curve, g2); }
+
+// R1CS arrays: rp/wire/coeff for L, R, O
+static R1csView make_r1cs(size_t nc, size_t nb_wires, size_t nb_public, const uint32_t* const* rp,
+                          const uint32_t* const* wire, const uint8_t* const* coeff) {
+  R1csView v;
+  v.nc = nc;
+  v.nb_wires = nb_wires;
+  v.nb_public = nb_public;
+  for (int m = 0; m < 3; m++) {
+    v.rp[m] = rp[m];
+    v.wire[m] = wire[m];
+    v.coeff[m] = coeff[m];
+  }
+  return v;
+}
+
+// sizes[0..4] = n, nb_wires, nbA, nbB, nbK ; g1 = {alpha, beta, delta, A, B, Z, K};
+// g2 = {beta, delta, B}; inf = {infA, infB}; toxic = 5 Fr mont (t, alpha, beta, gamma, delta)
+int o_g16_setup(int curve, size_t nc, size_t nb_wires, size_t nb_public, const uint32_t* const* rp,
+                const uint32_t* const* wire, const uint8_t* const* coeff, const uint8_t* toxic,
+                const size_t* sizes, uint8_t* const* g1, uint8_t* const* g2, uint8_t* const* inf,
+                int nthreads) {
+  R1csView rv = make_r1cs(nc, nb_wires, nb_public, rp, wire, coeff);
+  auto run = [&](auto tag) {
+    using C = decltype(tag);
+    Toxic<C> tw;
+    using Fr = typename C::Fr;
+    tw.t = load_fe<Fr>(toxic);
+    tw.alpha = load_fe<Fr>(toxic + 32);
+    tw.beta = load_fe<Fr>(toxic + 64);
+    tw.gamma = load_fe<Fr>(toxic + 96);
+    tw.delta = load_fe<Fr>(toxic + 128);
+    PkView<C> pk;
+    pk.n = sizes[0];
+    pk.nb_wires = sizes[1];
+    pk.nbA = sizes[2];
+    pk.nbB = sizes[3];
+    pk.nbK = sizes[4];
+    pk.g1_alpha = g1[0];
+    pk.g1_beta = g1[1];
+    pk.g1_delta = g1[2];
+    pk.g1_A = g1[3];
+    pk.g1_B = g1[4];
+    pk.g1_Z = g1[5];
+    pk.g1_K = g1[6];
+    pk.g2_beta = g2[0];
+    pk.g2_delta = g2[1];
+    pk.g2_B = g2[2];
+    pk.infA = inf[0];
+    pk.infB = inf[1];
+    return g16_setup<C>(rv, tw, pk, nthreads);
+  };
+  if (curve == 0) return run(BN{});
+  if (curve == 1) return run(BLS{});
+  return -1;
+}
+
+int o_g16_prove(int curve, const size_t* sizes, uint8_t* const* g1, uint8_t* const* g2,
+                uint8_t* const* inf, size_t nb_public, const uint8_t* wires, const uint8_t* a,
+                const uint8_t* b, const uint8_t* c, size_t nc, const uint8_t* r, const uint8_t* s,
+                int nthreads, uint8_t* ar, uint8_t* bs, uint8_t* krs) {
+  auto run = [&](auto tag) {
+    using C = decltype(tag);
+    PkView<C> pk;
+    pk.n = sizes[0];
+    pk.nb_wires = sizes[1];
+    pk.nbA = sizes[2];
+    pk.nbB = sizes[3];
+    pk.nbK = sizes[4];
+    pk.g1_alpha = g1[0];
+    pk.g1_beta = g1[1];
+    pk.g1_delta = g1[2];
+    pk.g1_A = g1[3];
+    pk.g1_B = g1[4];
+    pk.g1_Z = g1[5];
+    pk.g1_K = g1[6];
+    pk.g2_beta = g2[0];
+    pk.g2_delta = g2[1];
+    pk.g2_B = g2[2];
+    pk.infA = inf[0];
+    pk.infB = inf[1];
+    return g16_prove<C>(pk, nb_public, wires, a, b, c, nc, r, s, nthreads, ar, bs, krs);
+  };
+  if (curve == 0) return run(BN{});
+  if (curve == 1) return run(BLS{});
+  return -1;
+}
+
+int o_g16_check(int curve, size_t nc, size_t nb_wires, size_t nb_public, const uint32_t* const* rp,
+                const uint32_t* const* wire, const uint8_t* const* coeff, const uint8_t* toxic,
+                const uint8_t* wires, const uint8_t* r, const uint8_t* s, const uint8_t* ar,
+                const uint8_t* bs, const uint8_t* krs) {
+  R1csView rv = make_r1cs(nc, nb_wires, nb_public, rp, wire, coeff);
+  auto run = [&](auto tag) {
+    using C = decltype(tag);
+    using Fr = typename C::Fr;
+    Toxic<C> tw;
+    tw.t = load_fe<Fr>(toxic);
+    tw.alpha = load_fe<Fr>(toxic + 32);
+    tw.beta = load_fe<Fr>(toxic + 64);
+    tw.gamma = load_fe<Fr>(toxic + 96);
+    tw.delta = load_fe<Fr>(toxic + 128);
+    return g16_check<C>(rv, tw, wires, r, s, ar, bs, krs);
+  };
+  if (curve == 0) return run(BN{});
+  if (curve == 1) return run(BLS{});
+  return -1;
+}
+
+}  // extern "C"
+

@@ -1,0 +1,105 @@
+"""Test circuits in R1CS (CSR) form, with their solved witnesses.
+
+Shapes follow gnark's r1cs builder (frontend/cs/r1cs/api.go:199-212 -- one R1C
+per Mul of two non-constant variables; api_assertions.go:30-44 -- AssertIsEqual
+emits `1 * i1 == i2`) and the solver's wire order (constraint/bn254/solver.go:
+73-119: ONE wire, public, secret, internal):
+
+  * cubic_circuit()      examples/cubic/cubic.go:23-36 (x^3 + x + 5 == y), X=3, Y=35
+  * squaring_chain(k)    backend/groth16/groth16_test.go:120-156 (refCircuit): k squarings of X
+                         and AssertIsEqual(X_k, Y) -> k+1 constraints.
+
+Solve (constraint/bn254/solver.go:426-532) is outside the hot path; the helpers
+here compute the same W, a, b, c vectors directly for these circuits.
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+import pyref  # noqa: E402  (test oracle)
+
+
+class R1CS:
+    def __init__(self, curve: str, nb_public: int, nb_wires: int, constraints):
+        """constraints: list of (L, R, O), each a list of (wire, coeff:int)."""
+        self.curve = curve
+        self.c = pyref.CURVES[curve]
+        self.nb_public = nb_public
+        self.nb_wires = nb_wires
+        self.cons = constraints
+        self.nc = len(constraints)
+        n = 1
+        while n < self.nc:
+            n <<= 1
+        self.domain_size = n
+        self.rowptr, self.wires, self.coeffs = [], [], []
+        for m in range(3):
+            rp = [0]
+            ws, cs = [], []
+            for con in constraints:
+                for w, co in con[m]:
+                    ws.append(w)
+                    cs.append(pyref.encode_fr(self.c, co))
+                rp.append(len(ws))
+            self.rowptr.append(np.array(rp, dtype=np.uint32))
+            self.wires.append(np.array(ws if ws else [0], dtype=np.uint32))
+            self.coeffs.append(np.frombuffer(b"".join(cs) if cs else bytes(32), dtype=np.uint8).copy())
+        usedA = set(w for con in constraints for w, _ in con[0])
+        usedB = set(w for con in constraints for w, _ in con[1])
+        # exact infinity test happens in setup; for these circuits a wire is
+        # non-zero in A(t) iff it appears in some L (coefficients are non-zero)
+        self.nbA = len(usedA)
+        self.nbB = len(usedB)
+
+    def solve_abc(self, W):
+        r = self.c.r
+        a, b, cc = [], [], []
+        for L, R, O in self.cons:
+            a.append(sum(W[w] * co for w, co in L) % r)
+            b.append(sum(W[w] * co for w, co in R) % r)
+            cc.append(sum(W[w] * co for w, co in O) % r)
+        return a, b, cc
+
+    def is_satisfied(self, W):
+        a, b, cc = self.solve_abc(W)
+        return all(x * y % self.c.r == z for x, y, z in zip(a, b, cc))
+
+
+def cubic_circuit(curve: str = "bn254"):
+    # wires: 0 ONE, 1 Y (public), 2 X (secret), 3 t1 = X*X, 4 t2 = t1*X
+    cons = [
+        ([(2, 1)], [(2, 1)], [(3, 1)]),
+        ([(3, 1)], [(2, 1)], [(4, 1)]),
+        ([(0, 1)], [(1, 1)], [(4, 1), (2, 1), (0, 5)]),
+    ]
+    r1 = R1CS(curve, nb_public=2, nb_wires=5, constraints=cons)
+    X = 3
+    W = [1, 35, X, X * X, X * X * X]
+    return r1, W
+
+
+def squaring_chain(k: int, curve: str = "bn254", x: int = 2):
+    # wires: 0 ONE, 1 Y, 2 X, 3..3+k-1 internals w_1..w_k
+    cons = []
+    for j in range(k):
+        wj = 2 + j
+        cons.append(([(wj, 1)], [(wj, 1)], [(wj + 1, 1)]))
+    cons.append(([(0, 1)], [(2 + k, 1)], [(1, 1)]))
+    r1 = R1CS(curve, nb_public=2, nb_wires=3 + k, constraints=cons)
+    r = pyref.CURVES[curve].r
+    W = [1, 0, x % r]
+    v = x % r
+    for _ in range(k):
+        v = v * v % r
+        W.append(v)
+    W[1] = v
+    return r1, W
+
+
+def encode_vec(curve: str, vals) -> bytes:
+    c = pyref.CURVES[curve]
+    return b"".join(pyref.encode_fr(c, v) for v in vals)
