@@ -1,0 +1,182 @@
+// Device-side elliptic-curve arithmetic for the MSM bucket phase (gfx950).
+//
+// Curves: short Weierstrass y^2 = x^3 + b (a = 0) -- BN254 / BLS12-377, G1 over
+// Fp and G2 over Fp2.  Points arrive in gnark-crypto's G1Affine / G2Affine memory
+// layout ({X, Y}, Montgomery limbs, infinity encoded as (0,0)).
+//
+// Buckets are kept in XYZZ coordinates (x = X/ZZ, y = Y/ZZZ, ZZ^3 = ZZZ^2):
+//   mixed add  (madd-2008-s)   8M + 2S
+//   add        (add-2008-s)   12M + 2S
+//   double     (dbl-2008-s-1)  6M + 3S
+// (hyperelliptic.org EFD, "g1p/auto-shortw-xyzz").  Infinity is ZZ = 0.
+#pragma once
+#include "field.hpp"
+
+namespace gm {
+
+// ---- field-op dispatch for Fe<P> and Fe2<P,B> -------------------------------
+template <class F>
+struct FOps;
+
+template <class P>
+struct FOps<Fe<P>> {
+  using T = Fe<P>;
+  GM_DEV static T zero() { return fe_zero<P>(); }
+  GM_DEV static T one() { return fe_one<P>(); }
+};
+template <class P, int B>
+struct FOps<Fe2<P, B>> {
+  using T = Fe2<P, B>;
+  GM_DEV static T zero() { return {fe_zero<P>(), fe_zero<P>()}; }
+  GM_DEV static T one() { return {fe_one<P>(), fe_zero<P>()}; }
+};
+
+template <class F>
+struct Affine {
+  F x, y;
+};
+template <class F>
+struct XYZZ {
+  F x, y, zz, zzz;
+};
+
+template <class F>
+GM_DEV bool aff_is_inf(const Affine<F>& p) {
+  return fe_is_zero(p.x) && fe_is_zero(p.y);
+}
+
+template <class F>
+GM_DEV XYZZ<F> xyzz_inf() {
+  XYZZ<F> r;
+  r.x = FOps<F>::one();
+  r.y = FOps<F>::one();
+  r.zz = FOps<F>::zero();
+  r.zzz = FOps<F>::zero();
+  return r;
+}
+template <class F>
+GM_DEV bool xyzz_is_inf(const XYZZ<F>& p) {
+  return fe_is_zero(p.zz);
+}
+
+// 2*P for affine P (mdbl-2008-s-1); P must not be infinity.
+template <class F>
+GM_DEV XYZZ<F> xyzz_dbl_aff(const Affine<F>& p) {
+  F U = fe_dbl(p.y);
+  F V = fe_sqr(U);
+  F W = fe_mul(U, V);
+  F S = fe_mul(p.x, V);
+  F X2 = fe_sqr(p.x);
+  F M = fe_add(fe_dbl(X2), X2);
+  XYZZ<F> r;
+  r.x = fe_sub(fe_sqr(M), fe_dbl(S));
+  r.y = fe_sub(fe_mul(M, fe_sub(S, r.x)), fe_mul(W, p.y));
+  r.zz = V;
+  r.zzz = W;
+  return r;
+}
+
+// a += p, p affine (infinity allowed: skipped).
+template <class F>
+GM_DEV void xyzz_add_aff(XYZZ<F>& a, const Affine<F>& p) {
+  if (aff_is_inf(p)) return;
+  if (xyzz_is_inf(a)) {
+    a.x = p.x;
+    a.y = p.y;
+    a.zz = FOps<F>::one();
+    a.zzz = FOps<F>::one();
+    return;
+  }
+  F U2 = fe_mul(p.x, a.zz);
+  F S2 = fe_mul(p.y, a.zzz);
+  F P = fe_sub(U2, a.x);
+  F R = fe_sub(S2, a.y);
+  if (fe_is_zero(P)) {
+    if (fe_is_zero(R)) {
+      a = xyzz_dbl_aff(p);
+    } else {
+      a = xyzz_inf<F>();
+    }
+    return;
+  }
+  F PP = fe_sqr(P);
+  F PPP = fe_mul(P, PP);
+  F Q = fe_mul(a.x, PP);
+  F X3 = fe_sub(fe_sub(fe_sqr(R), PPP), fe_dbl(Q));
+  F Y3 = fe_sub(fe_mul(R, fe_sub(Q, X3)), fe_mul(a.y, PPP));
+  a.zz = fe_mul(a.zz, PP);
+  a.zzz = fe_mul(a.zzz, PPP);
+  a.x = X3;
+  a.y = Y3;
+}
+
+// 2*a (dbl-2008-s-1, a = 0).  Infinity maps to infinity (ZZ3 = V*0).
+template <class F>
+GM_DEV XYZZ<F> xyzz_dbl(const XYZZ<F>& a) {
+  F U = fe_dbl(a.y);
+  F V = fe_sqr(U);
+  F W = fe_mul(U, V);
+  F S = fe_mul(a.x, V);
+  F X2 = fe_sqr(a.x);
+  F M = fe_add(fe_dbl(X2), X2);
+  XYZZ<F> r;
+  r.x = fe_sub(fe_sqr(M), fe_dbl(S));
+  r.y = fe_sub(fe_mul(M, fe_sub(S, r.x)), fe_mul(W, a.y));
+  r.zz = fe_mul(V, a.zz);
+  r.zzz = fe_mul(W, a.zzz);
+  return r;
+}
+
+// a + b (add-2008-s) with all special cases.
+template <class F>
+GM_DEV XYZZ<F> xyzz_add(const XYZZ<F>& a, const XYZZ<F>& b) {
+  if (xyzz_is_inf(a)) return b;
+  if (xyzz_is_inf(b)) return a;
+  F U1 = fe_mul(a.x, b.zz);
+  F U2 = fe_mul(b.x, a.zz);
+  F S1 = fe_mul(a.y, b.zzz);
+  F S2 = fe_mul(b.y, a.zzz);
+  F P = fe_sub(U2, U1);
+  F R = fe_sub(S2, S1);
+  if (fe_is_zero(P)) {
+    if (fe_is_zero(R)) return xyzz_dbl(a);
+    return xyzz_inf<F>();
+  }
+  F PP = fe_sqr(P);
+  F PPP = fe_mul(P, PP);
+  F Q = fe_mul(U1, PP);
+  XYZZ<F> r;
+  r.x = fe_sub(fe_sub(fe_sqr(R), PPP), fe_dbl(Q));
+  r.y = fe_sub(fe_mul(R, fe_sub(Q, r.x)), fe_mul(S1, PPP));
+  r.zz = fe_mul(fe_mul(a.zz, b.zz), PP);
+  r.zzz = fe_mul(fe_mul(a.zzz, b.zzz), PPP);
+  return r;
+}
+
+template <class F>
+GM_DEV Affine<F> aff_neg(const Affine<F>& p) {
+  Affine<F> r;
+  r.x = p.x;
+  r.y = fe_neg(p.y);
+  return r;
+}
+
+// [k]a for a small non-negative integer k (< 2^32), double-and-add from the top.
+template <class F>
+GM_DEV XYZZ<F> xyzz_mul_small(const XYZZ<F>& a, uint32_t k) {
+  XYZZ<F> r = xyzz_inf<F>();
+  if (k == 0) return r;
+  int top = 31 - __builtin_clz(k);
+  r = a;
+  for (int b = top - 1; b >= 0; b--) {
+    r = xyzz_dbl(r);
+    if ((k >> b) & 1) r = xyzz_add(r, a);
+  }
+  return r;
+}
+
+// Curve bundles ---------------------------------------------------------------
+using Bn254Fp2 = Fe2<Bn254Fp, -1>;
+using Bls377Fp2 = Fe2<Bls377Fp, -5>;
+
+}  // namespace gm

@@ -40,6 +40,15 @@ namespace gm {
       constexpr uint32_t a[NLIMBS] = GM_##TAG##_R2_32;                            \
       return a[i];                                                                \
     }                                                                             \
+    /* limbs of p - 2 (Fermat exponent), borrow propagated */                     \
+    GM_HD static constexpr uint32_t pm2(int i) {                                  \
+      uint64_t borrow = 2;                                                        \
+      for (int k = 0;; k++) {                                                     \
+        const uint64_t v = (uint64_t)p(k) - borrow;                               \
+        if (k == i) return (uint32_t)v;                                           \
+        borrow = (v >> 63) & 1;                                                   \
+      }                                                                           \
+    }                                                                             \
   };
 
 GM_DEFINE_FIELD(Bn254Fp, BN254_FP, 8)
@@ -148,6 +157,8 @@ GM_DEV Fe<P> fe_neg(const Fe<P>& a) {
 }
 
 // CIOS Montgomery multiplication, no-carry variant (requires p.msw < 2^31-1).
+// Plain C: the compiler owns every carry and inserts the gfx950 VALU->carry
+// hazard padding itself.
 template <class P>
 GM_DEV Fe<P> fe_mul(const Fe<P>& a, const Fe<P>& b) {
   constexpr int N = P::N;
@@ -156,7 +167,6 @@ GM_DEV Fe<P> fe_mul(const Fe<P>& a, const Fe<P>& b) {
   for (int j = 0; j < N; j++) t[j] = 0;
 #pragma unroll
   for (int i = 0; i < N; i++) {
-    // t += a * b[i]
     uint64_t acc = (uint64_t)a.v[0] * b.v[i] + t[0];
     t[0] = (uint32_t)acc;
     uint32_t C = (uint32_t)(acc >> 32);
@@ -167,7 +177,6 @@ GM_DEV Fe<P> fe_mul(const Fe<P>& a, const Fe<P>& b) {
       C = (uint32_t)(acc >> 32);
     }
     const uint32_t A = C;
-    // reduction step
     const uint32_t m = t[0] * P::INV;
     acc = (uint64_t)m * P::p(0) + t[0];
     C = (uint32_t)(acc >> 32);
@@ -182,6 +191,54 @@ GM_DEV Fe<P> fe_mul(const Fe<P>& a, const Fe<P>& b) {
   Fe<P> r;
 #pragma unroll
   for (int j = 0; j < N; j++) r.v[j] = t[j];
+  fe_reduce_once(r);
+  return r;
+}
+
+// acc(64) += a*b with the carry out of the 64-bit accumulator added to hi.
+// v_mad_u64_u32 reports that carry in an SGPR pair; v_addc_co_u32 folds it in.
+GM_DEV void mad_acc(uint32_t a, uint32_t b, uint64_t& acc, uint32_t& hi) {
+  uint64_t c;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(c) : "v"(a), "v"(b));
+  asm("v_addc_co_u32 %0, %1, %2, 0, %3" : "=v"(hi), "=s"(c) : "v"(hi), "s"(c));
+}
+GM_DEV void mad_acc_s(uint32_t a, uint32_t b_uniform, uint64_t& acc, uint32_t& hi) {
+  uint64_t c;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(c) : "v"(a), "s"(b_uniform));
+  asm("v_addc_co_u32 %0, %1, %2, 0, %3" : "=v"(hi), "=s"(c) : "v"(hi), "s"(c));
+}
+
+// Finely-integrated product-scanning (FIPS) Montgomery multiplication:
+// column k accumulates a_i*b_{k-i} and m_i*p_{k-i} into a 64-bit accumulator
+// plus a carry word; 2N^2 v_mad_u64_u32 and no per-row carry propagation.
+// EXPERIMENTAL / NOT USED: the carry hand-off between the two asm statements
+// is a VALU-SGPR-write -> VALU-carry-read hazard that needs 2 wait states on
+// gfx950, but hipcc only pads 1 around inline asm -> intermittent stale
+// carries.  Kept for the microbenchmark until a hazard-safe form exists.
+template <class P>
+GM_DEV Fe<P> fe_mul_fips_asm(const Fe<P>& a, const Fe<P>& b) {
+  constexpr int N = P::N;
+  uint32_t m[N];
+  Fe<P> r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * N - 1; k++) {
+    uint32_t hi = 0;
+#pragma unroll
+    for (int i = (k - N + 1 > 0 ? k - N + 1 : 0); i <= (k < N - 1 ? k : N - 1); i++)
+      mad_acc(a.v[i], b.v[k - i], acc, hi);
+#pragma unroll
+    for (int i = (k - N + 1 > 0 ? k - N + 1 : 0); i <= (k - 1 < N - 1 ? k - 1 : N - 1); i++)
+      mad_acc_s(m[i], P::p(k - i), acc, hi);
+    if (k < N) {
+      m[k] = (uint32_t)acc * P::INV;
+      mad_acc_s(m[k], P::p(0), acc, hi);
+    } else {
+      r.v[k - N] = (uint32_t)acc;
+    }
+    acc = (acc >> 32) | ((uint64_t)hi << 32);
+  }
+  r.v[N - 1] = (uint32_t)acc;
   fe_reduce_once(r);
   return r;
 }
@@ -206,6 +263,20 @@ GM_DEV Fe<P> fe_to_mont(const Fe<P>& a) {
 #pragma unroll
   for (int i = 0; i < P::N; i++) r2.v[i] = P::r2(i);
   return fe_mul(a, r2);
+}
+
+// a^(p-2) (Fermat inversion; 0 -> 0).
+template <class P>
+GM_DEV Fe<P> fe_inv(const Fe<P>& a) {
+  Fe<P> r = fe_one<P>();
+  for (int i = P::N - 1; i >= 0; i--) {
+    const uint32_t e = P::pm2(i);
+    for (int b = 31; b >= 0; b--) {
+      r = fe_sqr(r);
+      if ((e >> b) & 1) r = fe_mul(r, a);
+    }
+  }
+  return r;
 }
 
 // ---------------------------------------------------------------------------
@@ -272,7 +343,12 @@ GM_DEV Fe2<P, BETA> fe_sqr(const Fe2<P, BETA>& a) {
   return r;
 }
 
-template <class F>
-struct FieldOps;  // (unused placeholder for traits if needed)
+template <class P, int BETA>
+GM_DEV Fe2<P, BETA> fe_inv(const Fe2<P, BETA>& a) {
+  // 1/(a0 + a1 u) = (a0 - a1 u) / (a0^2 - BETA a1^2)
+  Fe<P> nrm = fe_sub(fe_sqr(a.a0), mul_by_beta<P, BETA>(fe_sqr(a.a1)));
+  Fe<P> ni = fe_inv(nrm);
+  return {fe_mul(a.a0, ni), fe_neg(fe_mul(a.a1, ni))};
+}
 
 }  // namespace gm

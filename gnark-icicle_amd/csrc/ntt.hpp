@@ -1,0 +1,18 @@
+// NTT / computeH entry points (see ntt.hip).
+#pragma once
+#include <cstddef>
+#include "curves.hpp"
+
+struct gm_ctx;
+
+namespace gm {
+template <class C>
+int ntt_device(gm_ctx* ctx, void* data, size_t n, bool inverse, bool dit, bool coset);
+template <class C>
+int poly_ops_device(gm_ctx* ctx, void* a, const void* b, const void* c, size_t n, const void* den_host);
+template <class C>
+int reverse_device(gm_ctx* ctx, void* a, size_t n);
+template <class C>
+int compute_h_device(gm_ctx* ctx, void* a, void* b, void* c, size_t len, size_t n);
+void ntt_domains_free(gm_ctx* ctx);
+}  // namespace gm

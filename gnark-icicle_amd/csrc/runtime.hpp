@@ -1,0 +1,168 @@
+// Runtime plumbing for the C-ABI library: per-device context, stream, error
+// reporting, workspace allocation and per-kernel HIP-event profiling.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/gnark_mi355x.h"
+
+namespace gm {
+
+void set_error(const std::string& msg);
+
+#define GM_HIP(call)                                                                      \
+  do {                                                                                    \
+    hipError_t _e = (call);                                                               \
+    if (_e != hipSuccess) {                                                               \
+      ::gm::set_error(std::string(#call) + ": " + hipGetErrorString(_e) + " @" __FILE__ \
+                      ":" + std::to_string(__LINE__));                                    \
+      return GM_ERR_DEVICE;                                                               \
+    }                                                                                     \
+  } while (0)
+
+struct KernelStat {
+  double total_ms = 0;
+  uint64_t count = 0;
+};
+
+}  // namespace gm
+
+struct gm_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::recursive_mutex mu;
+  // per-kernel profiling with HIP events on this context's stream
+  bool profiling = false;
+  struct Pending {
+    std::string name;
+    hipEvent_t a, b;
+  };
+  std::vector<Pending> pending;
+  std::vector<hipEvent_t> event_pool;
+  std::map<std::string, gm::KernelStat> stats;
+  // cached NTT domains: key = curve*64 + logn
+  std::map<int, void*> ntt_domains;
+  int msm_c_override = 0;
+  // workspace arena: chunks of hipMalloc'd memory, stack-discipline scopes
+  struct Chunk {
+    char* base;
+    size_t cap;
+  };
+  std::vector<Chunk> chunks;
+  size_t cur_chunk = 0, cur_top = 0;
+};
+
+namespace gm {
+
+// Records a kernel launch bracketed by events when profiling is enabled.
+struct ProfScope {
+  gm_ctx* ctx;
+  const char* name;
+  hipEvent_t a = nullptr, b = nullptr;
+  ProfScope(gm_ctx* c, const char* n) : ctx(c), name(n) {
+    if (!ctx->profiling) return;
+    a = take();
+    b = take();
+    hipEventRecord(a, ctx->stream);
+  }
+  ~ProfScope() {
+    if (!ctx->profiling) return;
+    hipEventRecord(b, ctx->stream);
+    ctx->pending.push_back({name, a, b});
+  }
+  hipEvent_t take() {
+    if (!ctx->event_pool.empty()) {
+      hipEvent_t e = ctx->event_pool.back();
+      ctx->event_pool.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    hipEventCreate(&e);
+    return e;
+  }
+};
+
+// Drain finished profiling records (call after stream synchronisation).
+inline void prof_collect(gm_ctx* ctx) {
+  for (auto& p : ctx->pending) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+      auto& s = ctx->stats[p.name];
+      s.total_ms += ms;
+      s.count += 1;
+    }
+    ctx->event_pool.push_back(p.a);
+    ctx->event_pool.push_back(p.b);
+  }
+  ctx->pending.clear();
+}
+
+// Workspace arena scope.  All scratch of one API call is carved from the
+// context's chunk list with a bump pointer and released (LIFO) when the scope
+// ends.  Chunks stay allocated for reuse by later calls (no per-call
+// hipMalloc / hipFree on the hot path).  Calls on a context are serialised and
+// stream-synchronous, so a released range is never still in use by a kernel.
+struct Arena {
+  gm_ctx* ctx;
+  size_t saved_chunk, saved_top;
+  explicit Arena(gm_ctx* c) : ctx(c), saved_chunk(c->cur_chunk), saved_top(c->cur_top) {}
+  ~Arena() {
+    ctx->cur_chunk = saved_chunk;
+    ctx->cur_top = saved_top;
+  }
+  Arena(const Arena&) = delete;
+  Arena& operator=(const Arena&) = delete;
+  int alloc(size_t bytes, void** out) {
+    bytes = (bytes + 255) & ~size_t(255);
+    if (bytes == 0) bytes = 256;
+    while (ctx->cur_chunk < ctx->chunks.size()) {
+      auto& ch = ctx->chunks[ctx->cur_chunk];
+      if (ctx->cur_top + bytes <= ch.cap) {
+        *out = ch.base + ctx->cur_top;
+        ctx->cur_top += bytes;
+        return GM_OK;
+      }
+      ctx->cur_chunk++;
+      ctx->cur_top = 0;
+    }
+    size_t cap = bytes;
+    size_t last = ctx->chunks.empty() ? 0 : ctx->chunks.back().cap;
+    if (cap < 2 * last) cap = 2 * last;
+    if (cap < (size_t(64) << 20)) cap = size_t(64) << 20;
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, cap);
+    if (e != hipSuccess) {
+      // retry with the exact size
+      e = hipMalloc(&p, bytes);
+      cap = bytes;
+      if (e != hipSuccess) {
+        set_error(std::string("workspace hipMalloc(") + std::to_string(bytes) + "): " + hipGetErrorString(e));
+        return GM_ERR_OOM;
+      }
+    }
+    ctx->chunks.push_back({(char*)p, cap});
+    ctx->cur_chunk = ctx->chunks.size() - 1;
+    ctx->cur_top = bytes;
+    *out = p;
+    return GM_OK;
+  }
+};
+
+// A typed view of one arena allocation.
+struct DevBuf {
+  void* p = nullptr;
+  int alloc(Arena& a, size_t bytes) { return a.alloc(bytes, &p); }
+  template <class T>
+  T* as() const {
+    return reinterpret_cast<T*>(p);
+  }
+};
+
+inline unsigned blocks_for(size_t n, unsigned tpb) { return (unsigned)((n + tpb - 1) / tpb); }
+
+}  // namespace gm

@@ -1,0 +1,120 @@
+// Element-wise test hooks for the device field / curve layer (used by the
+// parity tests to pin each arithmetic primitive against the oracle).  Not on
+// the proving path.
+#include "curves.hpp"
+#include "runtime.hpp"
+
+namespace gm {
+
+template <class F>
+struct ElemIO {
+  GM_DEV static F load(const uint8_t* p, size_t i) {
+    F r;
+    memcpy(&r, p + sizeof(F) * i, sizeof(F));
+    return r;
+  }
+  GM_DEV static void store(uint8_t* p, size_t i, const F& v) { memcpy(p + sizeof(F) * i, &v, sizeof(F)); }
+};
+
+template <class F>
+__global__ void k_field_op(int op, const uint8_t* a, const uint8_t* b, uint8_t* out, size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  F x = ElemIO<F>::load(a, i), y = ElemIO<F>::load(b, i), r;
+  switch (op) {
+    case 0: r = fe_mul(x, y); break;
+    case 1: r = fe_add(x, y); break;
+    case 2: r = fe_sub(x, y); break;
+    case 3: r = fe_neg(x); break;
+    case 4: r = fe_inv(x); break;
+    case 5: r = fe_sqr(x); break;
+    default: r = x; break;
+  }
+  ElemIO<F>::store(out, i, r);
+}
+
+template <class F>
+GM_DEV Affine<F> to_affine_dev(const XYZZ<F>& a) {
+  Affine<F> r;
+  if (xyzz_is_inf(a)) {
+    r.x = FOps<F>::zero();
+    r.y = FOps<F>::zero();
+    return r;
+  }
+  F t = fe_inv(fe_mul(a.zz, a.zzz));
+  r.x = fe_mul(a.x, fe_mul(t, a.zzz));
+  r.y = fe_mul(a.y, fe_mul(t, a.zz));
+  return r;
+}
+
+template <class F>
+GM_DEV XYZZ<F> from_affine_dev(const Affine<F>& p) {
+  XYZZ<F> r = xyzz_inf<F>();
+  xyzz_add_aff(r, p);
+  return r;
+}
+
+template <class F>
+__global__ void k_point_op(int op, const Affine<F>* a, const Affine<F>* b, Affine<F>* out, size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Affine<F> p = a[i], q = b[i];
+  XYZZ<F> r;
+  switch (op) {
+    case 0: r = from_affine_dev(p); xyzz_add_aff(r, q); break;          // mixed add
+    case 1: r = xyzz_dbl(from_affine_dev(p)); break;                      // double
+    case 2: r = xyzz_add(from_affine_dev(p), from_affine_dev(q)); break;  // full add
+    case 3: r = xyzz_mul_small(from_affine_dev(p), 1000003u); break;      // small scalar mul
+    default: r = from_affine_dev(p); break;
+  }
+  out[i] = to_affine_dev(r);
+}
+
+}  // namespace gm
+
+using namespace gm;
+
+extern "C++" {
+template <class C>
+static int field_op_t(gm_ctx* ctx, int kind, int op, const void* a, const void* b, void* out, size_t n) {
+  auto g = dim3(blocks_for(n, 64)), t = dim3(64);
+  auto A = (const uint8_t*)a, B = (const uint8_t*)b;
+  auto O = (uint8_t*)out;
+  if (kind == 0) hipLaunchKernelGGL(k_field_op<Fe<typename C::Fr>>, g, t, 0, ctx->stream, op, A, B, O, n);
+  else if (kind == 1) hipLaunchKernelGGL(k_field_op<typename C::G1F>, g, t, 0, ctx->stream, op, A, B, O, n);
+  else hipLaunchKernelGGL(k_field_op<typename C::G2F>, g, t, 0, ctx->stream, op, A, B, O, n);
+  GM_HIP(hipGetLastError());
+  GM_HIP(hipStreamSynchronize(ctx->stream));
+  return GM_OK;
+}
+template <class C, bool G2>
+static int point_op_t(gm_ctx* ctx, int op, const void* a, const void* b, void* out, size_t n) {
+  using DF = typename GroupSel<C, G2>::DF;
+  hipLaunchKernelGGL(k_point_op<DF>, dim3(blocks_for(n, 64)), dim3(64), 0, ctx->stream, op,
+                     (const Affine<DF>*)a, (const Affine<DF>*)b, (Affine<DF>*)out, n);
+  GM_HIP(hipGetLastError());
+  GM_HIP(hipStreamSynchronize(ctx->stream));
+  return GM_OK;
+}
+}
+
+extern "C" {
+int gm_test_field_op(gm_ctx* ctx, int curve, int kind, int op, const void* a_dev, const void* b_dev,
+                     void* out_dev, size_t n) {
+  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  GM_HIP(hipSetDevice(ctx->device));
+  if (kind < 0 || kind > 2) return GM_ERR_INVALID;
+  return curve == GM_BN254 ? field_op_t<CurveBN254>(ctx, kind, op, a_dev, b_dev, out_dev, n)
+                           : field_op_t<CurveBLS12377>(ctx, kind, op, a_dev, b_dev, out_dev, n);
+}
+int gm_test_point_op(gm_ctx* ctx, int curve, int g2, int op, const void* a_dev, const void* b_dev,
+                     void* out_dev, size_t n) {
+  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  GM_HIP(hipSetDevice(ctx->device));
+  if (curve == GM_BN254)
+    return g2 ? point_op_t<CurveBN254, true>(ctx, op, a_dev, b_dev, out_dev, n)
+              : point_op_t<CurveBN254, false>(ctx, op, a_dev, b_dev, out_dev, n);
+  return g2 ? point_op_t<CurveBLS12377, true>(ctx, op, a_dev, b_dev, out_dev, n)
+            : point_op_t<CurveBLS12377, false>(ctx, op, a_dev, b_dev, out_dev, n);
+}
+}

@@ -1,0 +1,380 @@
+"""Python binding of libgnark_mi355x.so (ctypes) -- host plumbing for tests and
+bench.py.  The product is the C-ABI in include/gnark_mi355x.h; this module only
+mirrors it, keeping iciclegnark's operation names
+(backend/groth16/bn254/icicle/icicle.go call sites) so tests read like the
+reference's own flow:
+
+    CopyToDevice          -> copy_to_device            (icicle.go:44,47,65,245,269,352,478-480)
+    CopyPointsToDevice    -> copy_points_to_device     (icicle.go:90,95,109,114)
+    CopyG2PointsToDevice  -> copy_points_to_device(g2=True)  (icicle.go:125)
+    GenerateTwiddleFactors-> generate_twiddle_factors  (icicle.go:68,73)
+    INttOnDevice          -> intt_on_device            (icicle.go:489,502)
+    NttOnDevice           -> ntt_on_device             (icicle.go:490)
+    PolyOps               -> poly_ops                  (icicle.go:500)
+    ReverseScalars        -> reverse_scalars           (icicle.go:510)
+    MsmOnDevice           -> msm_on_device             (icicle.go:302,315,332,355)
+    MsmG2OnDevice         -> msm_g2_on_device          (icicle.go:382)
+    FreeDevicePointer     -> free_device_pointer       (icicle.go:356,416-418,492,505-507)
+    icicle_bn254.Prove    -> ProvingKey.prove          (icicle.go:133-422)
+
+There is NO fallback: if the shared library is missing or no GPU is visible the
+calls raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libgnark_mi355x.so")
+
+BN254, BLS12_377 = 0, 1
+CURVES = {"bn254": BN254, "bls12377": BLS12_377}
+FP_BYTES = {BN254: 32, BLS12_377: 48}
+FR_BYTES = 32
+
+# exported symbols (include/gnark_mi355x.h) -- checked by tests/test_capi_symbols.py
+SYMBOLS = [
+    "gm_last_error", "gm_version", "gm_init", "gm_destroy", "gm_synchronize",
+    "gm_profile_enable", "gm_profile_reset", "gm_profile_get", "gm_profile_dump",
+    "gm_set_msm_window", "gm_malloc", "gm_free", "gm_copy_to_device", "gm_memcpy_h2d",
+    "gm_memcpy_d2h", "gm_copy_points_to_device", "gm_msm", "gm_msm_host_scalars", "gm_ntt",
+    "gm_poly_ops", "gm_reverse_scalars", "gm_groth16_compute_h", "gm_g16_pk_upload",
+    "gm_g16_pk_free", "gm_g16_prove", "gm_g16_prove_device", "gm_jac_add", "gm_jac_to_affine",
+    "gm_batch_mul_base", "gm_random_scalars", "gm_generator", "gm_test_field_op",
+    "gm_test_point_op",
+]
+
+
+class GmError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Loads the C-ABI library (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise GmError(f"{path} not built -- run `make -C gnark-icicle_amd` (or __graft_entry__.build())")
+    L = ctypes.CDLL(path)
+    vp, sz, i, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
+    pvp = ctypes.POINTER(ctypes.c_void_p)
+    L.gm_last_error.restype = ctypes.c_char_p
+    L.gm_init.argtypes = [i, pvp]
+    L.gm_destroy.argtypes = [vp]
+    L.gm_synchronize.argtypes = [vp]
+    L.gm_profile_enable.argtypes = [vp, i]
+    L.gm_profile_reset.argtypes = [vp]
+    L.gm_profile_get.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64)]
+    L.gm_profile_dump.argtypes = [vp, ctypes.c_char_p, sz]
+    L.gm_set_msm_window.argtypes = [vp, i]
+    L.gm_malloc.argtypes = [vp, sz, pvp]
+    L.gm_free.argtypes = [vp, vp]
+    L.gm_copy_to_device.argtypes = [vp, vp, sz, pvp]
+    L.gm_memcpy_h2d.argtypes = [vp, vp, vp, sz]
+    L.gm_memcpy_d2h.argtypes = [vp, vp, vp, sz]
+    L.gm_copy_points_to_device.argtypes = [vp, i, i, vp, sz, pvp]
+    L.gm_msm.argtypes = [vp, i, i, vp, vp, sz, vp, vp]
+    L.gm_msm_host_scalars.argtypes = [vp, i, i, vp, vp, sz, vp, vp]
+    L.gm_ntt.argtypes = [vp, i, vp, sz, i, i, i]
+    L.gm_poly_ops.argtypes = [vp, i, vp, vp, vp, sz, vp]
+    L.gm_reverse_scalars.argtypes = [vp, i, vp, sz]
+    L.gm_groth16_compute_h.argtypes = [vp, i, vp, vp, vp, sz, sz]
+    L.gm_g16_pk_upload.argtypes = [vp, i, vp, pvp]
+    L.gm_g16_pk_free.argtypes = [vp, vp]
+    L.gm_g16_prove.argtypes = [vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, vp, vp]
+    L.gm_g16_prove_device.argtypes = [vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, vp, vp]
+    L.gm_jac_add.argtypes = [i, i, vp, vp, vp]
+    L.gm_jac_to_affine.argtypes = [i, i, vp, vp]
+    L.gm_batch_mul_base.argtypes = [vp, i, i, vp, vp, sz, vp]
+    L.gm_random_scalars.argtypes = [vp, i, u64, sz, vp]
+    L.gm_generator.argtypes = [i, i, vp]
+    L.gm_test_field_op.argtypes = [vp, i, i, i, vp, vp, vp, sz]
+    L.gm_test_point_op.argtypes = [vp, i, i, i, vp, vp, vp, sz]
+    _lib = L
+    return L
+
+
+def _check(rc: int):
+    if rc != 0:
+        raise GmError(f"gnark_mi355x error {rc}: {load_library().gm_last_error().decode()}")
+
+
+def _buf(b) -> np.ndarray:
+    if isinstance(b, np.ndarray):
+        return np.ascontiguousarray(b).view(np.uint8).reshape(-1)
+    return np.frombuffer(bytes(b), dtype=np.uint8)
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def curve_id(curve) -> int:
+    return CURVES[curve] if isinstance(curve, str) else int(curve)
+
+
+def point_bytes(curve, g2: bool) -> int:
+    return FP_BYTES[curve_id(curve)] * (4 if g2 else 2)
+
+
+def jac_bytes(curve, g2: bool) -> int:
+    return FP_BYTES[curve_id(curve)] * (6 if g2 else 3)
+
+
+def generator(curve, g2: bool = False) -> bytes:
+    out = np.zeros(point_bytes(curve, g2), np.uint8)
+    _check(load_library().gm_generator(curve_id(curve), int(g2), _p(out)))
+    return out.tobytes()
+
+
+def jac_add(curve, g2: bool, p: bytes, q: bytes) -> bytes:
+    out = np.zeros(jac_bytes(curve, g2), np.uint8)
+    a, b = _buf(p), _buf(q)
+    _check(load_library().gm_jac_add(curve_id(curve), int(g2), _p(a), _p(b), _p(out)))
+    return out.tobytes()
+
+
+def jac_to_affine(curve, g2: bool, p: bytes) -> bytes:
+    out = np.zeros(point_bytes(curve, g2), np.uint8)
+    a = _buf(p)
+    _check(load_library().gm_jac_to_affine(curve_id(curve), int(g2), _p(a), _p(out)))
+    return out.tobytes()
+
+
+class DeviceBuffer:
+    """A device allocation owned by a Context (OnDeviceData{P, Size}, icicle.go:228)."""
+
+    def __init__(self, ctx: "Context", ptr: int, nbytes: int):
+        self.ctx, self.ptr, self.nbytes = ctx, ptr, nbytes
+
+    def to_host(self, nbytes: int | None = None) -> bytes:
+        n = self.nbytes if nbytes is None else nbytes
+        out = np.zeros(n, np.uint8)
+        _check(load_library().gm_memcpy_d2h(self.ctx.handle, _p(out), self.ptr, n))
+        return out.tobytes()
+
+    def write(self, data, offset: int = 0):
+        a = _buf(data)
+        _check(load_library().gm_memcpy_h2d(self.ctx.handle, self.ptr + offset, _p(a), a.size))
+
+    def free(self):
+        if self.ptr:
+            _check(load_library().gm_free(self.ctx.handle, self.ptr))
+            self.ptr = 0
+
+
+class Context:
+    """One HIP device + stream (gm_ctx)."""
+
+    def __init__(self, device: int = 0):
+        L = load_library()
+        h = ctypes.c_void_p()
+        _check(L.gm_init(device, ctypes.byref(h)))
+        self.handle = h
+        self.device = device
+
+    def close(self):
+        if self.handle:
+            load_library().gm_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---- memory ----------------------------------------------------------
+    def malloc(self, nbytes: int) -> DeviceBuffer:
+        p = ctypes.c_void_p()
+        _check(load_library().gm_malloc(self.handle, nbytes, ctypes.byref(p)))
+        return DeviceBuffer(self, p.value, nbytes)
+
+    def copy_to_device(self, data) -> DeviceBuffer:
+        a = _buf(data)
+        p = ctypes.c_void_p()
+        _check(load_library().gm_copy_to_device(self.handle, _p(a), a.size, ctypes.byref(p)))
+        return DeviceBuffer(self, p.value, a.size)
+
+    def copy_points_to_device(self, curve, points, g2: bool = False) -> DeviceBuffer:
+        a = _buf(points)
+        n = a.size // point_bytes(curve, g2)
+        p = ctypes.c_void_p()
+        _check(load_library().gm_copy_points_to_device(self.handle, curve_id(curve), int(g2), _p(a), n,
+                                                       ctypes.byref(p)))
+        return DeviceBuffer(self, p.value, a.size)
+
+    def free_device_pointer(self, buf: DeviceBuffer):
+        buf.free()
+
+    def synchronize(self):
+        _check(load_library().gm_synchronize(self.handle))
+
+    # ---- profiling ---------------------------------------------------------
+    def profile(self, on: bool = True):
+        _check(load_library().gm_profile_enable(self.handle, int(on)))
+
+    def profile_reset(self):
+        _check(load_library().gm_profile_reset(self.handle))
+
+    def profile_stats(self) -> dict:
+        buf = ctypes.create_string_buffer(1 << 16)
+        _check(load_library().gm_profile_dump(self.handle, buf, len(buf)))
+        out = {}
+        for line in buf.value.decode().splitlines():
+            name, ms, cnt = line.split()
+            out[name] = (float(ms), int(cnt))
+        return out
+
+    def set_msm_window(self, c: int):
+        _check(load_library().gm_set_msm_window(self.handle, c))
+
+    # ---- MSM -----------------------------------------------------------------
+    def msm(self, curve, scalars: DeviceBuffer, points: DeviceBuffer, n: int, g2: bool = False):
+        """Returns (jacobian_bytes, affine_bytes) in gnark layout."""
+        jac = np.zeros(jac_bytes(curve, g2), np.uint8)
+        aff = np.zeros(point_bytes(curve, g2), np.uint8)
+        sp = scalars.ptr if isinstance(scalars, DeviceBuffer) else scalars
+        pp = points.ptr if isinstance(points, DeviceBuffer) else points
+        _check(load_library().gm_msm(self.handle, curve_id(curve), int(g2), sp, pp, n, _p(jac), _p(aff)))
+        return jac.tobytes(), aff.tobytes()
+
+    def msm_on_device(self, scalars, points, n, curve="bn254"):
+        """MsmOnDevice(scalars_d, points_d, count, convert=true) -> G1Jac bytes."""
+        return self.msm(curve, scalars, points, n, g2=False)[0]
+
+    def msm_g2_on_device(self, scalars, points, n, curve="bn254"):
+        """MsmG2OnDevice -> G2Jac bytes."""
+        return self.msm(curve, scalars, points, n, g2=True)[0]
+
+    # ---- NTT -----------------------------------------------------------------
+    def ntt(self, curve, data: DeviceBuffer, n: int, inverse: bool, dit: bool, coset: bool):
+        _check(load_library().gm_ntt(self.handle, curve_id(curve), data.ptr, n, int(inverse), int(dit),
+                                     int(coset)))
+
+    def generate_twiddle_factors(self, curve, n: int, inverse: bool = False):
+        """Twiddle tables are built and cached per (curve, n) inside the context on
+        first use; this warms that cache (GenerateTwiddleFactors)."""
+        tmp = self.malloc(FR_BYTES * n)
+        try:
+            _check(load_library().gm_ntt(self.handle, curve_id(curve), tmp.ptr, n, int(inverse), 0, 0))
+        finally:
+            tmp.free()
+
+    def poly_ops(self, curve, a: DeviceBuffer, b: DeviceBuffer, c: DeviceBuffer, n: int, den: bytes):
+        d = _buf(den)
+        _check(load_library().gm_poly_ops(self.handle, curve_id(curve), a.ptr, b.ptr, c.ptr, n, _p(d)))
+
+    def reverse_scalars(self, curve, data: DeviceBuffer, n: int):
+        _check(load_library().gm_reverse_scalars(self.handle, curve_id(curve), data.ptr, n))
+
+    def compute_h(self, curve, a: DeviceBuffer, b: DeviceBuffer, c: DeviceBuffer, length: int, n: int):
+        _check(load_library().gm_groth16_compute_h(self.handle, curve_id(curve), a.ptr, b.ptr, c.ptr,
+                                                   length, n))
+
+    # ---- synthetic inputs ---------------------------------------------------
+    def random_scalars(self, curve, n: int, seed: int) -> DeviceBuffer:
+        buf = self.malloc(FR_BYTES * n)
+        _check(load_library().gm_random_scalars(self.handle, curve_id(curve), seed, n, buf.ptr))
+        return buf
+
+    def batch_mul_base(self, curve, g2: bool, base: bytes, scalars: DeviceBuffer, n: int) -> DeviceBuffer:
+        out = self.malloc(point_bytes(curve, g2) * n)
+        b = _buf(base)
+        _check(load_library().gm_batch_mul_base(self.handle, curve_id(curve), int(g2), _p(b), scalars.ptr,
+                                                n, out.ptr))
+        return out
+
+
+    # ---- test hooks ---------------------------------------------------------
+    def test_field_op(self, curve, kind: int, op: int, a: bytes, b: bytes) -> bytes:
+        A, B = self.copy_to_device(a), self.copy_to_device(b)
+        O = self.malloc(len(a))
+        esz = {0: 32, 1: FP_BYTES[curve_id(curve)], 2: 2 * FP_BYTES[curve_id(curve)]}[kind]
+        try:
+            _check(load_library().gm_test_field_op(self.handle, curve_id(curve), kind, op, A.ptr, B.ptr, O.ptr,
+                                                   len(a) // esz))
+            return O.to_host()
+        finally:
+            for x in (A, B, O):
+                x.free()
+
+    def test_point_op(self, curve, g2: bool, op: int, a: bytes, b: bytes) -> bytes:
+        A, B = self.copy_to_device(a), self.copy_to_device(b)
+        O = self.malloc(len(a))
+        try:
+            _check(load_library().gm_test_point_op(self.handle, curve_id(curve), int(g2), op, A.ptr, B.ptr,
+                                                   O.ptr, len(a) // point_bytes(curve, g2)))
+            return O.to_host()
+        finally:
+            for x in (A, B, O):
+                x.free()
+
+
+# ---------------------------------------------------------------------------
+# Groth16 (icicle_bn254 ProvingKey / Prove mirror)
+# ---------------------------------------------------------------------------
+class _PkHost(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_size_t) for k in ["domain_size", "nb_wires", "nb_public", "nbA", "nbB", "nbK"]] + \
+               [(k, ctypes.c_void_p) for k in ["g1_alpha", "g1_beta", "g1_delta", "g1_A", "g1_B", "g1_Z", "g1_K",
+                                                "g2_beta", "g2_delta", "g2_B", "infA", "infB"]]
+
+
+class ProvingKey:
+    """Device-resident Groth16 proving key (icicle_bn254.ProvingKey + deviceInfo,
+    provingkey.go:10-28; uploaded once like setupDevicePointers, icicle.go:31-130).
+
+    `pk` is a dict of gnark-layout byte arrays: g1_alpha, g1_beta, g1_delta, g1_A,
+    g1_B, g1_Z (n-1, bit-reversed), g1_K, g2_beta, g2_delta, g2_B, infA, infB.
+    """
+
+    def __init__(self, ctx: Context, curve, pk: dict, domain_size: int, nb_wires: int, nb_public: int):
+        self.ctx = ctx
+        self.curve = curve_id(curve)
+        g1b = point_bytes(curve, False)
+        arrs = {k: _buf(v) for k, v in pk.items() if k != "sizes"}
+        h = _PkHost()
+        h.domain_size, h.nb_wires, h.nb_public = domain_size, nb_wires, nb_public
+        h.nbA = arrs["g1_A"].size // g1b
+        h.nbB = arrs["g1_B"].size // g1b
+        h.nbK = arrs["g1_K"].size // g1b
+        for k in ["g1_alpha", "g1_beta", "g1_delta", "g1_A", "g1_B", "g1_Z", "g1_K", "g2_beta", "g2_delta",
+                  "g2_B", "infA", "infB"]:
+            setattr(h, k, arrs[k].ctypes.data)
+        self._keep = arrs
+        handle = ctypes.c_void_p()
+        _check(load_library().gm_g16_pk_upload(ctx.handle, self.curve, ctypes.byref(h), ctypes.byref(handle)))
+        self.handle = handle
+        self.n, self.nb_wires, self.nb_public = domain_size, nb_wires, nb_public
+
+    def free(self):
+        if self.handle:
+            load_library().gm_g16_pk_free(self.ctx.handle, self.handle)
+            self.handle = None
+
+    def prove(self, wires, a, b, c, r: bytes, s: bytes):
+        """Returns (Ar, Bs, Krs) affine bytes (gnark layout)."""
+        W, A, B, C, R, S = (_buf(x) for x in (wires, a, b, c, r, s))
+        ar = np.zeros(point_bytes(self.curve, False), np.uint8)
+        krs = np.zeros(point_bytes(self.curve, False), np.uint8)
+        bs = np.zeros(point_bytes(self.curve, True), np.uint8)
+        _check(load_library().gm_g16_prove(self.ctx.handle, self.handle, _p(W), _p(A), _p(B), _p(C),
+                                           A.size // FR_BYTES, _p(R), _p(S), _p(ar), _p(bs), _p(krs)))
+        return ar.tobytes(), bs.tobytes(), krs.tobytes()
+
+    def prove_device(self, wires: DeviceBuffer, a: DeviceBuffer, b: DeviceBuffer, c: DeviceBuffer,
+                     nb_constraints: int, r: bytes, s: bytes):
+        R, S = _buf(r), _buf(s)
+        ar = np.zeros(point_bytes(self.curve, False), np.uint8)
+        krs = np.zeros(point_bytes(self.curve, False), np.uint8)
+        bs = np.zeros(point_bytes(self.curve, True), np.uint8)
+        _check(load_library().gm_g16_prove_device(self.ctx.handle, self.handle, wires.ptr, a.ptr, b.ptr, c.ptr,
+                                                  nb_constraints, _p(R), _p(S), _p(ar), _p(bs), _p(krs)))
+        return ar.tobytes(), bs.tobytes(), krs.tobytes()

@@ -1,0 +1,180 @@
+/*
+ * gnark_mi355x.h -- C-ABI of the MI355X (gfx950) MSM + NTT backend for gnark's
+ * Groth16 prover.  Drop-in replacement for the device layer that
+ * backend/groth16/bn254/icicle/icicle.go binds through
+ * github.com/ingonyama-zk/iciclegnark v0.1.0 (go.mod:15; not vendored -- the
+ * signatures below are the ones its call sites in icicle.go imply).
+ *
+ * Conventions
+ *  - Plain C, no torch / HIP types in signatures.  Device buffers are opaque
+ *    `void*` device pointers owned by the caller and released with gm_free
+ *    (iciclegnark's unsafe.Pointer + FreeDevicePointer model).
+ *  - Host pointers are only read/written during the call and never retained
+ *    (cgo rule).  Every entry point selects its context's device itself.
+ *  - Memory layout is gnark-crypto's, byte for byte: fr.Element / fp.Element =
+ *    little-endian u64 limbs in Montgomery form; G1Affine {X,Y}; G2Affine
+ *    {X.A0,X.A1,Y.A0,Y.A1}; G1Jac/G2Jac {X,Y,Z}; infinity affine = all zero.
+ *  - Every function returns GM_OK (0) or a negative gm_status; the message of
+ *    the last failure on the calling thread is available from gm_last_error().
+ *  - Calls on one context are serialised; use one context per thread/GPU for
+ *    concurrency (one process per GPU in multi-GPU jobs).
+ */
+#ifndef GNARK_MI355X_H
+#define GNARK_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  GM_OK = 0,
+  GM_ERR_INVALID = -1,     /* bad argument / unsupported size */
+  GM_ERR_DEVICE = -2,      /* HIP runtime error */
+  GM_ERR_OOM = -3,         /* device allocation failed */
+  GM_ERR_UNSUPPORTED = -4, /* curve/group combination not built */
+} gm_status;
+
+typedef enum { GM_BN254 = 0, GM_BLS12_377 = 1 } gm_curve;
+
+typedef struct gm_ctx gm_ctx;
+
+/* ---- context ---------------------------------------------------------- */
+const char* gm_last_error(void);
+int gm_version(void);
+/* Creates a context on HIP device `device` with its own stream. */
+int gm_init(int device, gm_ctx** out);
+int gm_destroy(gm_ctx* ctx);
+int gm_synchronize(gm_ctx* ctx);
+/* Per-kernel timing with HIP events on the context stream (bench/profiling). */
+int gm_profile_enable(gm_ctx* ctx, int on);
+int gm_profile_reset(gm_ctx* ctx);
+/* Fetches accumulated time (ms) and launch count for kernel `name`. */
+int gm_profile_get(gm_ctx* ctx, const char* name, double* total_ms, uint64_t* count);
+/* Writes "name total_ms count\n" lines into buf (truncated to cap). */
+int gm_profile_dump(gm_ctx* ctx, char* buf, size_t cap);
+/* Test/tuning knob: force the MSM window size c (0 = automatic). */
+int gm_set_msm_window(gm_ctx* ctx, int c);
+
+/* ---- memory (iciclegnark CopyToDevice / CopyPointsToDevice /
+ *      CopyG2PointsToDevice / FreeDevicePointer; icicle.go:44,47,65,90,95,
+ *      109,114,125,245,269,352,356,416-418,478-480,492,505-507) ---------- */
+int gm_malloc(gm_ctx* ctx, size_t bytes, void** dev_out);
+int gm_free(gm_ctx* ctx, void* dev);
+int gm_copy_to_device(gm_ctx* ctx, const void* host, size_t bytes, void** dev_out);
+int gm_memcpy_h2d(gm_ctx* ctx, void* dev, const void* host, size_t bytes);
+int gm_memcpy_d2h(gm_ctx* ctx, void* host, const void* dev, size_t bytes);
+/* Uploads n gnark affine points of (curve, g2) -> device buffer. */
+int gm_copy_points_to_device(gm_ctx* ctx, int curve, int g2, const void* host_points, size_t n,
+                             void** dev_out);
+
+/* ---- MSM (iciclegnark MsmOnDevice icicle.go:302,315,332,355 and
+ *      MsmG2OnDevice icicle.go:382; CPU twin G1Jac/G2Jac.MultiExp
+ *      prove.go:204,217,237,247,293) ------------------------------------
+ * out = sum_i int(scalars[i]) * points[i], scalars = n Montgomery fr.Element,
+ * points = n gnark affine points ((0,0) = infinity is allowed), both resident
+ * on the device.  out_jac receives gnark's G1Jac (3 x fp) / G2Jac (3 x E2)
+ * layout; out_affine (optional, may be NULL) receives the affine form. */
+int gm_msm(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const void* points_dev,
+           size_t n, void* out_jac, void* out_affine);
+/* Same with scalars in host memory (copied on the context stream). */
+int gm_msm_host_scalars(gm_ctx* ctx, int curve, int g2, const void* scalars_host,
+                        const void* points_dev, size_t n, void* out_jac, void* out_affine);
+
+/* ---- NTT (iciclegnark GenerateTwiddleFactors icicle.go:68,73;
+ *      INttOnDevice :489,502; NttOnDevice :490; PolyOps :500;
+ *      ReverseScalars :510; CPU twin fft.Domain.FFT/FFTInverse
+ *      prove.go:372-378,396) ---------------------------------------------
+ * In-place transform of n = 2^k Montgomery fr.Elements with gnark-crypto
+ * fft.Domain semantics:
+ *   inverse = 0: coefficients -> evaluations at w^i (g*w^i if coset)
+ *   inverse = 1: evaluations -> coefficients, scaled by 1/n (and g^-i if coset)
+ *   dit = 0 (DIF): natural-order input, bit-reversed output
+ *   dit = 1 (DIT): bit-reversed input, natural-order output
+ * w = the domain generator of fft.NewDomain(n), g = FrMultiplicativeGen
+ * (5 for BN254, 22 for BLS12-377). */
+int gm_ntt(gm_ctx* ctx, int curve, void* data_dev, size_t n, int inverse, int dit, int coset);
+/* a[i] <- (a[i]*b[i] - c[i]) * den   (PolyOps, den = (g^n - 1)^-1 broadcast) */
+int gm_poly_ops(gm_ctx* ctx, int curve, void* a_dev, const void* b_dev, const void* c_dev,
+                size_t n, const void* den_host);
+/* In-place bit-reversal permutation of n = 2^k Fr elements (ReverseScalars). */
+int gm_reverse_scalars(gm_ctx* ctx, int curve, void* data_dev, size_t n);
+
+/* ---- Groth16 computeH (icicle.go:453-513; prove.go:356-399) -----------
+ * a, b, c: `len` Montgomery fr.Elements each (the R1CS solution vectors),
+ * device-resident, zero-padded in place to n = domain size (buffers must hold
+ * n elements).  On return a_dev holds h in BIT-REVERSED coefficient order
+ * (matching pk.G1.Z, setup.go:265-267); b_dev and c_dev are clobbered. */
+int gm_groth16_compute_h(gm_ctx* ctx, int curve, void* a_dev, void* b_dev, void* c_dev,
+                         size_t len, size_t n);
+
+/* ---- Groth16 prover (icicle_bn254.Prove, icicle.go:133-422; CPU twin
+ *      groth16_bn254.Prove prove.go:62-325, without the BSB22 commitment
+ *      side path) ---------------------------------------------------------
+ * A proving key whose point arrays live on the device (uploaded once, as
+ * icicle's setupDevicePointers, icicle.go:31-130). */
+typedef struct gm_g16_pk gm_g16_pk;
+typedef struct {
+  size_t domain_size;      /* n = pk.Domain.Cardinality */
+  size_t nb_wires;         /* len(InfinityA) */
+  size_t nb_public;        /* r1cs.GetNbPublicVariables() (incl. ONE wire) */
+  size_t nbA, nbB, nbK;    /* len(pk.G1.A), len(pk.G1.B), len(pk.G1.K) */
+  const void* g1_alpha;    /* G1Affine */
+  const void* g1_beta;
+  const void* g1_delta;
+  const void* g1_A;        /* nbA points */
+  const void* g1_B;        /* nbB points */
+  const void* g1_Z;        /* n-1 points, bit-reversed (setup.go:265-267) */
+  const void* g1_K;        /* nbK points */
+  const void* g2_beta;     /* G2Affine */
+  const void* g2_delta;
+  const void* g2_B;        /* nbB points */
+  const uint8_t* infA;     /* nb_wires flags (InfinityA) */
+  const uint8_t* infB;     /* nb_wires flags (InfinityB) */
+} gm_g16_pk_host;
+
+int gm_g16_pk_upload(gm_ctx* ctx, int curve, const gm_g16_pk_host* pk, gm_g16_pk** out);
+int gm_g16_pk_free(gm_ctx* ctx, gm_g16_pk* pk);
+
+/* Proves with solved vectors in host memory: wires (nb_wires Fr), a, b, c
+ * (nb_constraints Fr each), r and s (one Fr each, Montgomery).  Outputs
+ * proof.Ar (G1Affine), proof.Bs (G2Affine), proof.Krs (G1Affine). */
+int gm_g16_prove(gm_ctx* ctx, gm_g16_pk* pk, const void* wires, const void* a, const void* b,
+                 const void* c, size_t nb_constraints, const void* r, const void* s,
+                 void* ar_out, void* bs_out, void* krs_out);
+/* Same with wires/a/b/c already resident on the device (a, b, c buffers hold
+ * n elements and are clobbered). */
+int gm_g16_prove_device(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, void* a_dev,
+                        void* b_dev, void* c_dev, size_t nb_constraints, const void* r,
+                        const void* s, void* ar_out, void* bs_out, void* krs_out);
+
+/* ---- host-side group helpers (finishing adds of sharded MSMs) ---------- */
+/* out = p + q, all gnark Jacobian (G1Jac or G2Jac). */
+int gm_jac_add(int curve, int g2, const void* p, const void* q, void* out);
+/* affine_out = p in affine form. */
+int gm_jac_to_affine(int curve, int g2, const void* p, void* affine_out);
+
+/* ---- synthetic inputs (bench / tests; not on the hot path) ------------
+ * out[i] = [k_i] base, k_i = Montgomery fr.Elements on the device, outputs
+ * affine points on the device (curve.BatchScalarMultiplicationG1/G2). */
+int gm_batch_mul_base(gm_ctx* ctx, int curve, int g2, const void* base_affine_host,
+                      const void* scalars_dev, size_t n, void* points_out_dev);
+/* Fills n Montgomery Fr elements uniform in [0, r) from a seed (device). */
+int gm_random_scalars(gm_ctx* ctx, int curve, uint64_t seed, size_t n, void* scalars_dev);
+/* Generator points of the curve in gnark affine layout (host). */
+int gm_generator(int curve, int g2, void* affine_out);
+
+/* ---- test hooks (element-wise device primitives; parity tests only) ---
+ * kind: 0 = Fr, 1 = Fp, 2 = Fp2; op: 0 mul, 1 add, 2 sub, 3 neg, 4 inv, 5 sqr.
+ * Point op (affine in/out): 0 mixed add, 1 double, 2 XYZZ add, 3 [1000003]P. */
+int gm_test_field_op(gm_ctx* ctx, int curve, int kind, int op, const void* a_dev,
+                     const void* b_dev, void* out_dev, size_t n);
+int gm_test_point_op(gm_ctx* ctx, int curve, int g2, int op, const void* a_dev,
+                     const void* b_dev, void* out_dev, size_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GNARK_MI355X_H */

@@ -1,0 +1,131 @@
+"""MSM parity: HIP Pippenger (gm_msm, replaces iciclegnark MsmOnDevice /
+MsmG2OnDevice, icicle.go:302,315,332,355,382) vs the CPU oracle (restatement of
+gnark-crypto MultiExp, prove.go:204,217,237,247,293).  Bit-exact on the affine
+result (the affine form of a group element is unique)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import pyref
+
+pytestmark = pytest.mark.gpu
+
+CASES = [("bn254", False), ("bn254", True), ("bls12377", False), ("bls12377", True)]
+
+
+def _edge_inputs(cname, g2, n, seed):
+    c = pyref.CURVES[cname]
+    G = pyref.Group(c, g2)
+    pts = pyref.random_points(c, n, seed, g2)
+    sc = pyref.random_scalars(c, n, seed + 1)
+    # edge cases the reference meets: infinity (0,0) points (pk.K, icicle.go:98-105),
+    # scalars 0, 1, r-1, duplicate points (DummySetup, setup.go:544-558), P and -P
+    pts[1] = None
+    sc[2] = 0
+    sc[3] = 1
+    sc[4] = c.r - 1
+    pts[6] = pts[5]
+    sc[6] = sc[5]
+    pts[8] = G.neg(pts[7])
+    sc[8] = sc[7]
+    pts[10] = pts[9]
+    sc[10] = c.r - sc[9]
+    return sc, pts
+
+
+@pytest.mark.parametrize("cname,g2", CASES)
+def test_msm_small_vs_pyref(gm_ctx, cname, g2):
+    c = pyref.CURVES[cname]
+    n = 48
+    sc, pts = _edge_inputs(cname, g2, n, 1000 + 7 * g2)
+    exp = pyref.Group(c, g2).msm(sc, pts)
+    sb = b"".join(pyref.encode_fr(c, s) for s in sc)
+    pb = b"".join(pyref.encode_point(c, p, g2) for p in pts)
+    S = gm_ctx.copy_to_device(sb)
+    P = gm_ctx.copy_points_to_device(cname, pb, g2)
+    for window in (0, 4, 9):
+        gm_ctx.set_msm_window(window)
+        jac, aff = gm_ctx.msm(cname, S, P, n, g2)
+        assert pyref.decode_point(c, aff, g2) == exp, (cname, g2, window)
+    gm_ctx.set_msm_window(0)
+    S.free()
+    P.free()
+
+
+@pytest.mark.parametrize("cname,g2", CASES)
+def test_msm_empty_and_single(gm_ctx, cname, g2):
+    import gnark_mi355x as gm
+    c = pyref.CURVES[cname]
+    P0 = pyref.random_points(c, 1, 5, g2)[0]
+    S = gm_ctx.copy_to_device(pyref.encode_fr(c, 12345))
+    P = gm_ctx.copy_points_to_device(cname, pyref.encode_point(c, P0, g2), g2)
+    _, aff = gm_ctx.msm(cname, S, P, 0, g2)
+    assert aff == bytes(gm.point_bytes(cname, g2))  # empty MSM = infinity
+    _, aff = gm_ctx.msm(cname, S, P, 1, g2)
+    assert pyref.decode_point(c, aff, g2) == pyref.Group(c, g2).mul(P0, 12345)
+    S.free()
+    P.free()
+
+
+def test_msm_all_equal_points(gm_ctx, oracle):
+    """DummySetup shape (setup.go:544-558): every point identical -> every bucket
+    add is a doubling."""
+    c = pyref.BN254
+    n = 4096
+    P0 = pyref.random_points(c, 1, 77)[0]
+    pb = pyref.encode_point(c, P0, False) * n
+    sc = pyref.random_scalars(c, n, 78)
+    sb = b"".join(pyref.encode_fr(c, s) for s in sc)
+    S = gm_ctx.copy_to_device(sb)
+    P = gm_ctx.copy_points_to_device("bn254", pb)
+    _, aff = gm_ctx.msm("bn254", S, P, n)
+    assert aff == oracle.msm("bn254", False, sb, pb)
+    S.free()
+    P.free()
+
+
+@pytest.mark.parametrize("cname,g2,logn", [("bn254", False, 16), ("bn254", True, 13),
+                                           ("bls12377", False, 14), ("bls12377", True, 12)])
+def test_msm_random_vs_oracle(gm_ctx, oracle, cname, g2, logn):
+    import gnark_mi355x as gm
+    n = (1 << logn) + 37  # ragged size
+    S = gm_ctx.random_scalars(cname, n, seed=0x5EED0002 + logn)
+    K = gm_ctx.random_scalars(cname, n, seed=0x5EED1002 + logn)
+    P = gm_ctx.batch_mul_base(cname, g2, gm.generator(cname, g2), K, n)
+    sb = S.to_host()
+    pb = P.to_host()
+    _, aff = gm_ctx.msm(cname, S, P, n, g2)
+    assert aff == oracle.msm(cname, g2, sb, pb)
+    for b in (S, K, P):
+        b.free()
+
+
+def test_batch_mul_base_matches_oracle(gm_ctx, oracle):
+    import gnark_mi355x as gm
+    for cname in ("bn254", "bls12377"):
+        for g2 in (False, True):
+            K = gm_ctx.random_scalars(cname, 64, seed=99)
+            P = gm_ctx.batch_mul_base(cname, g2, gm.generator(cname, g2), K, 64)
+            assert P.to_host() == oracle.batch_mul_base(cname, g2, gm.generator(cname, g2), K.to_host())
+            K.free()
+            P.free()
+
+
+def test_msm_skewed_scalars(gm_ctx, oracle):
+    """Groth16 wire values are skewed (many 0/1/small values): one huge bucket."""
+    c = pyref.BN254
+    n = 1 << 14
+    rng = np.random.default_rng(5)
+    vals = [int(x) for x in rng.integers(0, 3, n)]
+    vals[::97] = [int(x) for x in rng.integers(0, 2**62, len(vals[::97]))]
+    sb = b"".join(pyref.encode_fr(c, v) for v in vals)
+    import gnark_mi355x as gm
+    K = gm_ctx.random_scalars("bn254", n, seed=3)
+    P = gm_ctx.batch_mul_base("bn254", False, gm.generator("bn254"), K, n)
+    S = gm_ctx.copy_to_device(sb)
+    _, aff = gm_ctx.msm("bn254", S, P, n)
+    assert aff == oracle.msm("bn254", False, sb, P.to_host())
+    for b in (S, K, P):
+        b.free()
