@@ -1,0 +1,261 @@
+#!/usr/bin/env python3
+"""Benchmark: BN254 G1 MSM throughput (BASELINE.json configs[1]: 2^20 random
+points/scalars per GPU) through the C-ABI of libgnark_mi355x.so, plus the
+secondary metrics the same BASELINE metric names (NTT Gelem/s at 2^24, Groth16
+prove time) on rank 0.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--logn 20]
+  torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+
+Multi-GPU = the MSM sharded by splitting the point/scalar array across ranks
+(weak scaling: every rank holds a fixed 2^logn shard); each step every rank runs
+its shard's Pippenger MSM, the per-rank partial sums (gnark G1Jac, 96 B) are
+all-gathered over RCCL and reduced by host EC adds.
+
+Inputs are resident in HBM before the timed region.  The cpu_baseline leg times
+the oracle's C++ Pippenger restatement (oracle/, "port", not gnark-crypto: no Go
+toolchain on the box) on the same workload on the host.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "gnark-icicle_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (8.0 TB/s spec)
+MSM_BYTES_PER_POINT = 96  # 64 B affine point + 32 B scalar
+NTT_BYTES_PER_ELEM = 64   # one 32 B read + one 32 B write per transform
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--logn", type=int, default=20, help="MSM points per GPU = 2^logn")
+    ap.add_argument("--ntt-logn", type=int, default=24)
+    ap.add_argument("--g16-logn", type=int, default=20, help="Groth16 prove domain (0 = skip)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true")
+    return ap.parse_args()
+
+
+def load_pmc_traffic(name):
+    """HBM bytes per launch from a committed rocprofv3 --pmc summary (or None)."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            return json.load(f).get(name)
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+    import gnark_mi355x as gm
+
+    ctx = gm.Context(local_rank)
+    n = 1 << args.logn
+    # ---- resident synthetic inputs: this rank's shard of the MSM ----------------
+    seed = 0x5EED0002 + rank
+    S = ctx.random_scalars("bn254", n, seed)
+    K = ctx.random_scalars("bn254", n, 0x5EED1002 + rank)
+    P = ctx.batch_mul_base("bn254", False, gm.generator("bn254"), K, n)
+    K.free()
+    ctx.synchronize()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def step():
+        jac, _ = ctx.msm("bn254", S, P, n)
+        if dist is not None:
+            t = torch.frombuffer(bytearray(jac), dtype=torch.uint8).cuda()
+            parts = [torch.empty_like(t) for _ in range(world)]
+            dist.all_gather(parts, t)
+            acc = parts[0].cpu().numpy().tobytes()
+            for q in parts[1:]:
+                acc = gm.jac_add("bn254", False, acc, q.cpu().numpy().tobytes())
+            jac = acc
+        return jac
+
+    for _ in range(args.warmup):
+        step()
+    ctx.profile_reset()
+    ctx.profile(True)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    barrier()
+    dt = time.perf_counter() - t0
+    ctx.profile(False)
+    stats = ctx.profile_stats()
+    if dist is not None:
+        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    ms_per_step = dt * 1e3 / args.steps
+    total_points = n * world
+    value = total_points / (dt / args.steps) / 1e6
+
+    # ---- roofline of the dominant kernel (bucket accumulation) ------------------
+    acc_ms, acc_cnt = stats.get("msm_accum_g1", (0.0, 0))
+    acc_avg_ms = acc_ms / max(acc_cnt, 1)
+    alg_bytes = MSM_BYTES_PER_POINT * n  # per launch: one MSM of n points
+    achieved_gbs = alg_bytes / (acc_avg_ms * 1e-3) / 1e9 if acc_avg_ms > 0 else 0.0
+    roofline = {
+        "kernel": "k_msm_accum<Fe<Bn254Fp>> (msm_accum_g1)",
+        "bound": "hbm",
+        "achieved": round(achieved_gbs, 2),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved_gbs / HBM_PEAK_GBS, 5),
+        "traffic": load_pmc_traffic("msm_accum_g1"),
+        "avg_launch_ms": round(acc_avg_ms, 4),
+        "note": "MSM is 32-bit integer-multiply bound (no MFMA); see DESIGN.md for the int-ALU roofline",
+    }
+    kernel_ms = {k: round(v[0] / max(v[1], 1), 4) for k, v in stats.items()}
+
+    out = {
+        "metric": "BN254 G1 MSM Mpoints/s (2^%d points per GPU, sharded MSM)" % args.logn,
+        "value": round(value, 3),
+        "unit": "Mpoints/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32 limbs (BN254 Fp/Fr Montgomery, integer)",
+        "data": "synthetic: uniform scalars, points [k_i]G1 (seeded)",
+        "config": {"workload": "BN254 G1 MSM 2^%d random points/scalars per GPU (BASELINE configs[1])" % args.logn,
+                   "points_per_gpu": n, "total_points": total_points, "parallelism": "msm-shard%d" % world},
+        "roofline": roofline,
+        "kernel_avg_ms": kernel_ms,
+    }
+
+    if rank == 0 and not args.no_secondary and world == 1:
+        out["secondary"] = secondary(ctx, gm, args)
+    if rank == 0 and not args.no_cpu_baseline and world == 1:
+        out["cpu_baseline"] = cpu_baseline(S, P, n, res)
+    if rank == 0:
+        print(json.dumps(out))
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def secondary(ctx, gm, args):
+    """NTT Gelem/s (config 3) and Groth16 prove time (configs 3/4) on this GPU."""
+    res = {}
+    nn = 1 << args.ntt_logn
+    X = ctx.random_scalars("bn254", nn, 7)
+    ctx.ntt("bn254", X, nn, 0, 0, 0)  # builds the domain tables (untimed)
+    ctx.ntt("bn254", X, nn, 1, 1, 0)
+    ctx.profile_reset()
+    ctx.profile(True)
+    reps = 5
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ctx.ntt("bn254", X, nn, 0, 0, 0)   # forward DIF
+        ctx.ntt("bn254", X, nn, 1, 1, 0)   # inverse DIT (round trip)
+    ctx.synchronize()
+    dt = (time.perf_counter() - t0) / (2 * reps)
+    ctx.profile(False)
+    st = ctx.profile_stats()
+    pass_ms, pass_cnt = st.get("ntt_pass", (0.0, 0))
+    avg_pass = pass_ms / max(pass_cnt, 1)
+    X.free()
+    gbs = NTT_BYTES_PER_ELEM * nn / dt / 1e9
+    res["ntt"] = {"logn": args.ntt_logn, "gelem_per_s": round(nn / dt / 1e9, 4), "ms_per_transform": round(dt * 1e3, 4),
+                  "achieved_gbs": round(gbs, 1), "frac_hbm": round(gbs / HBM_PEAK_GBS, 4),
+                  "avg_pass_ms": round(avg_pass, 4), "passes_per_transform": round(pass_cnt / (2 * reps), 2)}
+    if args.g16_logn:
+        res["groth16"] = groth16_bench(ctx, gm, args.g16_logn)
+    return res
+
+
+def groth16_bench(ctx, gm, logn):
+    """Groth16 prove at n = 2^logn with a synthetic proving key (random points,
+    the DummySetup-style timing setup of groth16_test.go:70-88) and synthetic
+    solution vectors; timer scope = icicle.go:204-412 (after Solve)."""
+    import numpy as np
+    n = 1 << logn
+    nb_wires = n + 2
+    nb_public = 2
+    gen1, gen2 = gm.generator("bn254", False), gm.generator("bn254", True)
+
+    def pts(count, g2, seed):
+        k = ctx.random_scalars("bn254", count, seed)
+        p = ctx.batch_mul_base("bn254", g2, gen2 if g2 else gen1, k, count)
+        b = p.to_host()
+        k.free()
+        p.free()
+        return np.frombuffer(b, np.uint8)
+
+    one1 = pts(3, False, 1)
+    one2 = pts(2, True, 2)
+    pk = {"g1_alpha": one1[:64], "g1_beta": one1[64:128], "g1_delta": one1[128:192],
+          "g1_A": pts(nb_wires, False, 3), "g1_B": pts(nb_wires, False, 4), "g1_Z": pts(n - 1, False, 5),
+          "g1_K": pts(nb_wires - nb_public, False, 6), "g2_beta": one2[:128], "g2_delta": one2[128:256],
+          "g2_B": pts(nb_wires, True, 7), "infA": np.zeros(nb_wires, np.uint8), "infB": np.zeros(nb_wires, np.uint8)}
+    dpk = gm.ProvingKey(ctx, "bn254", pk, n, nb_wires, nb_public)
+    W = ctx.random_scalars("bn254", nb_wires, 8)
+    A, B, C = (ctx.malloc(32 * n) for _ in range(3))
+    srcs = [ctx.random_scalars("bn254", n, 9 + i) for i in range(3)]
+    r = ctx.random_scalars("bn254", 2, 12).to_host()
+    times = []
+    for it in range(3):
+        for dst, src in zip((A, B, C), srcs):
+            dst.write(src.to_host())
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        dpk.prove_device(W, A, B, C, n, r[:32], r[32:])
+        times.append(time.perf_counter() - t0)
+    dpk.free()
+    for b in [W, A, B, C] + srcs:
+        b.free()
+    return {"logn": logn, "prove_ms": round(min(times) * 1e3, 3), "note": "inputs device-resident; after Solve"}
+
+
+def cpu_baseline(S, P, n, gpu_jac):
+    """Oracle C++ Pippenger (the 'port') on the host, same 2^logn workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_lib
+    threads = min(16, os.cpu_count() or 1)
+    sb, pb = S.to_host(), P.to_host()
+    oracle_lib.msm("bn254", False, sb[: 32 * 1024], pb[: 64 * 1024], nthreads=threads)  # warm
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        aff = oracle_lib.msm("bn254", False, sb, pb, nthreads=threads)
+        reps += 1
+        if time.perf_counter() - t0 > 10 or reps >= 3:
+            break
+    dt = (time.perf_counter() - t0) / reps
+    import gnark_mi355x as gm
+    match = gm.jac_to_affine("bn254", False, gpu_jac) == aff
+    return {"value": round(n / dt / 1e6, 4), "unit": "Mpoints/s", "cores": threads, "kind": "port",
+            "sample": "full 2^%d-point BN254 G1 MSM, %d rep(s), C++ Pippenger restatement (oracle/), not gnark-crypto"
+                      % (n.bit_length() - 1, reps),
+            "result_matches_gpu": bool(match)}
+
+
+if __name__ == "__main__":
+    main()

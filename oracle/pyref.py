@@ -464,3 +464,69 @@ def random_points(c: CurveParams, n: int, seed: int, g2: bool = False):
     rng = random.Random(seed)
     gen = G.generator()
     return [G.mul(gen, rng.randrange(1, c.r)) for _ in range(n)]
+
+
+# ----------------------------------------------------------------------------
+# Groth16 (small circuits only) -- setup.go:85-349 / prove.go:62-325 without
+# BSB22 commitments.  Constraints: list of (L, R, O) sparse rows [(wire, coeff)].
+# ----------------------------------------------------------------------------
+
+
+def g16_setup(c: CurveParams, cons, nb_wires: int, nb_public: int, toxic):
+    t, alpha, beta, gamma, delta = (x % c.r for x in toxic)
+    r = c.r
+    nc = len(cons)
+    n = 1
+    while n < nc:
+        n <<= 1
+    w = domain_generator(c, n)
+    A, B, C = [0] * nb_wires, [0] * nb_wires, [0] * nb_wires
+    tn1 = (pow(t, n, r) - 1) % r
+    ninv = pow(n, -1, r)
+    for j, (L, Rr, O) in enumerate(cons):
+        wj = pow(w, j, r)
+        lag = wj * tn1 * ninv * pow((t - wj) % r, -1, r) % r   # L_j(t)
+        for wi, co in L:
+            A[wi] = (A[wi] + co * lag) % r
+        for wi, co in Rr:
+            B[wi] = (B[wi] + co * lag) % r
+        for wi, co in O:
+            C[wi] = (C[wi] + co * lag) % r
+    dinv = pow(delta, -1, r)
+    G1, G2 = Group(c, False), Group(c, True)
+    g1, g2 = c.g1, c.g2
+    K = [(beta * A[i] + alpha * B[i] + C[i]) * dinv % r for i in range(nb_public, nb_wires)]
+    Z = [(pow(t, i, r) * tn1 * dinv) % r for i in range(n)]
+    infA = [a == 0 for a in A]
+    infB = [b == 0 for b in B]
+    Zp = [G1.mul(g1, z) for z in Z]
+    logn = n.bit_length() - 1
+    Zp = [Zp[bitrev(i, logn)] for i in range(n)][: n - 1]
+    return {
+        "n": n, "nb_wires": nb_wires, "nb_public": nb_public,
+        "g1_alpha": G1.mul(g1, alpha), "g1_beta": G1.mul(g1, beta), "g1_delta": G1.mul(g1, delta),
+        "g1_A": [G1.mul(g1, a) for a in A if a], "g1_B": [G1.mul(g1, b) for b in B if b],
+        "g1_Z": Zp, "g1_K": [G1.mul(g1, k) for k in K],
+        "g2_beta": G2.mul(g2, beta), "g2_delta": G2.mul(g2, delta),
+        "g2_B": [G2.mul(g2, b) for b in B if b],
+        "infA": infA, "infB": infB,
+    }
+
+
+def g16_prove(c: CurveParams, pk, wires, a, b, cc, r_: int, s_: int):
+    G1, G2 = Group(c, False), Group(c, True)
+    rr = c.r
+    n = pk["n"]
+    h = compute_h(c, a, b, cc, n)
+    wA = [v for v, inf in zip(wires, pk["infA"]) if not inf]
+    wB = [v for v, inf in zip(wires, pk["infB"]) if not inf]
+    kr = (-r_ * s_) % rr
+    delta = pk["g1_delta"]
+    ar = G1.add(G1.add(G1.msm(wA, pk["g1_A"]), pk["g1_alpha"]), G1.mul(delta, r_))
+    bs1 = G1.add(G1.add(G1.msm(wB, pk["g1_B"]), pk["g1_beta"]), G1.mul(delta, s_))
+    krs = G1.add(G1.msm(wires[pk["nb_public"]:], pk["g1_K"]), G1.mul(delta, kr))
+    krs = G1.add(krs, G1.msm(h[: n - 1], pk["g1_Z"]))
+    krs = G1.add(krs, G1.mul(ar, s_) if ar else None)
+    krs = G1.add(krs, G1.mul(bs1, r_) if bs1 else None)
+    bs = G2.add(G2.add(G2.msm(wB, pk["g2_B"]), G2.mul(pk["g2_delta"], s_)), pk["g2_beta"])
+    return ar, bs, krs

@@ -1,0 +1,65 @@
+"""End-to-end Groth16 parity: gm_g16_prove (HIP; replaces icicle_bn254.Prove,
+backend/groth16/bn254/icicle/icicle.go:133-422) vs the oracle's restatement of
+groth16_bn254.Prove (backend/groth16/bn254/prove.go:62-325) on the same pk,
+witness and (r, s) -- the proof elements Ar, Bs, Krs must be byte-identical
+(SURVEY.md §0.4), and must satisfy the verification equation in the exponent
+for the known toxic waste (equivalent of groth16.Verify, verify.go:49-150)."""
+import pytest
+
+import pyref
+import r1cs as R
+
+pytestmark = pytest.mark.gpu
+
+TOXIC = [0x1D5A2B3C4D5E6F708192A3B4C5D6E7F8091A2B3C4D5E6F708192A3B4C5D6E7,
+         0x2E6B3C4D5E6F708192A3B4C5D6E7F8091A2B3C4D5E6F708192A3B4C5D6E7F8,
+         0x3F7C4D5E6F708192A3B4C5D6E7F8091A2B3C4D5E6F708192A3B4C5D6E7F809,
+         0x0A8D5E6F708192A3B4C5D6E7F8091A2B3C4D5E6F708192A3B4C5D6E7F8091A,
+         0x1B9E6F708192A3B4C5D6E7F8091A2B3C4D5E6F708192A3B4C5D6E7F8091A2B]
+
+
+def _prove_both(gm_ctx, oracle, cname, r1, W, rr, ss):
+    import gnark_mi355x as gm
+    c = pyref.CURVES[cname]
+    tox = R.encode_vec(cname, [t % c.r for t in TOXIC])
+    pk = oracle.g16_setup(cname, r1, tox)
+    a, b, cc = r1.solve_abc(W)
+    enc = lambda v: R.encode_vec(cname, v)
+    rb, sb = enc([rr]), enc([ss])
+    exp = oracle.g16_prove(cname, pk, r1.nb_public, enc(W), enc(a), enc(b), enc(cc), rb, sb)
+    dpk = gm.ProvingKey(gm_ctx, cname, pk, r1.domain_size, r1.nb_wires, r1.nb_public)
+    try:
+        got = dpk.prove(enc(W), enc(a), enc(b), enc(cc), rb, sb)
+    finally:
+        dpk.free()
+    ok = oracle.g16_check(cname, r1, tox, enc(W), rb, sb, *got)
+    return exp, got, ok
+
+
+@pytest.mark.parametrize("cname", ["bn254", "bls12377"])
+def test_groth16_cubic(gm_ctx, oracle, cname):
+    """examples/cubic (BASELINE config 1 circuit) -- n = 4."""
+    r1, W = R.cubic_circuit(cname)
+    exp, got, ok = _prove_both(gm_ctx, oracle, cname, r1, W, 0x1234567, 0x7654321)
+    assert got == exp
+    assert ok == 7
+
+
+@pytest.mark.parametrize("cname,k", [("bn254", 15), ("bn254", 1023), ("bn254", 4000),
+                                     ("bls12377", 511)])
+def test_groth16_squaring_chain(gm_ctx, oracle, cname, k):
+    """refCircuit of backend/groth16/groth16_test.go:120-156 with k squarings."""
+    r1, W = R.squaring_chain(k, cname, x=2)
+    exp, got, ok = _prove_both(gm_ctx, oracle, cname, r1, W, 0xABCDEF0123, 0x13579BDF)
+    assert got == exp
+    assert ok == 7
+
+
+def test_groth16_rejects_bad_witness(gm_ctx, oracle):
+    """A proof from an unsatisfying witness must fail the exponent check."""
+    r1, W = R.squaring_chain(63, "bn254")
+    W = list(W)
+    W[10] = (W[10] + 1) % pyref.BN254.r
+    exp, got, ok = _prove_both(gm_ctx, oracle, "bn254", r1, W, 5, 7)
+    assert got == exp  # same (invalid) computation on both sides
+    assert ok != 7

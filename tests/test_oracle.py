@@ -1,0 +1,159 @@
+"""CPU tests of the oracle (no GPU): pins the restatements against the values
+the reference itself holds, then checks the C++ restatement against the
+pure-Python one and against the committed golden fixtures."""
+import glob
+import json
+import os
+
+import pytest
+
+import pyref
+import r1cs as R
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = os.path.join(HERE, "golden")
+
+
+def _load(name):
+    with open(os.path.join(GOLDEN, name + ".json")) as f:
+        return json.load(f)
+
+
+# ---- reference-pinned constants ------------------------------------------------
+
+def test_bn254_twist_vectors_from_reference():
+    """std/algebra/emulated/sw_bn254/pairing_test.go:333-345 (point NOT on the twist)
+    and :394-404 (point on the curve but NOT in G2)."""
+    c = pyref.BN254
+    G2 = pyref.Group(c, True)
+    not_on = ((0x119606e6d3ea97cea4eff54433f5c7dbc026b8d0670ddfbe6441e31225028d31,
+               0x1d3df5be6084324da6333a6ad1367091ca9fbceb70179ec484543a58b8cb5d63),
+              (0x1b9a36ea373fe2c5b713557042ce6deb2907d34e12be595f9bbe84c144de86ef,
+               0x49fe60975e8c78b7b31a6ed16a338ac8b28cf6a065cfd2ca47e9402882518ba0 % c.p))
+    assert not G2.on_curve(not_on)
+    on_not_sub = ((0x07192b9fd0e2a32e3e1caa8e59462b757326d48f641924e6a1d00d66478913eb,
+                   0x15ce93f1b1c4946dd6cfbb3d287d9c9a1cdedb264bda7aada0844416d8a47a63),
+                  (0x0fa65a9b48ba018361ed081e3b9e958451de5d9e8ae0bd251833ebb4b2fafc96,
+                   0x06e1f5e20f68f6dfa8a91a3bea048df66d9eaf56cc7f11215401f7e05027e0c6))
+    assert G2.on_curve(on_not_sub)
+    assert G2.mul(on_not_sub, c.r) is not None  # not in the r-torsion subgroup
+
+
+@pytest.mark.parametrize("cname", ["bn254", "bls12377"])
+def test_curve_constants(cname):
+    c = pyref.CURVES[cname]
+    for g2 in (False, True):
+        G = pyref.Group(c, g2)
+        assert G.on_curve(G.generator())
+        assert G.mul(G.generator(), c.r) is None
+    # 2-adic root of unity of exact order 2^s, = g^((r-1)/2^s)
+    w = c.omega_max
+    assert pow(w, 1 << c.two_adicity, c.r) == 1
+    assert pow(w, 1 << (c.two_adicity - 1), c.r) != 1
+    assert pow(c.coset_gen, (c.r - 1) >> c.two_adicity, c.r) == w
+
+
+def test_bn254_double_generator_kat():
+    """2*G1 for BN254 (SURVEY.md §8c known answer)."""
+    G = pyref.Group(pyref.BN254, False)
+    P = G.mul(G.generator(), 2)
+    assert P == (0x030644e72e131a029b85045b68181585d97816a916871ca8d3c208c16d87cfd3,
+                 0x15ed738c0e0a7c92e7845f96b2ae9c0a68a6a449e3538fc7ff3ebf7a5a18a2c4)
+
+
+def test_filter_heap_reference_vectors():
+    """backend/groth16/bn254/utils_test.go:17-38."""
+    e = [0, 1, 2, 3]
+    assert pyref.filter_heap(e, 0, [1, 2]) == [0, 3]
+    assert pyref.filter_heap(e[1:], 1, [1, 2]) == [3]
+    assert pyref.filter_heap(e, 0, [1, 1, 2]) == [0, 3]
+    assert pyref.filter_heap(e[1:], 1, [1, 1, 2]) == [3]
+
+
+def test_bitreverse_matches_setup():
+    """setup.go:690-700 bitReverse."""
+    assert pyref.bit_reverse(list(range(8))) == [0, 4, 2, 6, 1, 5, 3, 7]
+
+
+# ---- C++ restatement vs golden fixtures (pure-Python restatement outputs) ------
+
+@pytest.mark.parametrize("name", sorted(os.path.basename(p)[:-5] for p in glob.glob(os.path.join(GOLDEN, "msm_*.json"))))
+def test_oracle_msm_golden(oracle, name):
+    g = _load(name)
+    got = oracle.msm(g["curve"], g["g2"], bytes.fromhex(g["scalars"]), bytes.fromhex(g["points"]))
+    assert got.hex() == g["expected_affine"]
+    got = oracle.msm(g["curve"], g["g2"], bytes.fromhex(g["scalars"]), bytes.fromhex(g["points"]), naive=True)
+    assert got.hex() == g["expected_affine"]
+
+
+@pytest.mark.parametrize("cname", ["bn254", "bls12377"])
+def test_oracle_ntt_golden(oracle, cname):
+    g = _load("ntt_" + cname)
+    x = bytes.fromhex(g["input"])
+    for mode, exp in g["outputs"].items():
+        inverse, dit, coset = (int(ch) for ch in mode)
+        assert oracle.fft(cname, x, inverse, dit, coset).hex() == exp, mode
+
+
+@pytest.mark.parametrize("name", ["h_cubic_bn254", "h_cubic_bls12377", "h_squaring15_bn254",
+                                  "h_squaring15_bls12377"])
+def test_oracle_compute_h_golden(oracle, name):
+    g = _load(name)
+    got = oracle.compute_h(g["curve"], bytes.fromhex(g["a"]), bytes.fromhex(g["b"]), bytes.fromhex(g["c"]), g["n"])
+    assert got.hex() == g["h_bitrev"]
+
+
+def _pk_from_fixture(g):
+    import numpy as np
+    pk = {k: np.frombuffer(bytes.fromhex(v), np.uint8).copy() for k, v in g["pk"].items()}
+    fpb = 32 if g["curve"] == "bn254" else 48
+    nbK = g["nb_wires"] - g["nb_public"]
+    pk["sizes"] = np.array([g["n"], g["nb_wires"], len(pk["g1_A"]) // (2 * fpb), len(pk["g1_B"]) // (2 * fpb), nbK],
+                           dtype=np.uint64)
+    return pk
+
+
+@pytest.mark.parametrize("cname", ["bn254", "bls12377"])
+def test_oracle_groth16_golden(oracle, cname):
+    g = _load("groth16_cubic_" + cname)
+    pk = _pk_from_fixture(g)
+    h = lambda k: bytes.fromhex(g[k])
+    ar, bs, krs = oracle.g16_prove(cname, pk, g["nb_public"], h("wires"), h("a"), h("b"), h("c"), h("r"), h("s"))
+    assert (ar.hex(), bs.hex(), krs.hex()) == (g["expected"]["Ar"], g["expected"]["Bs"], g["expected"]["Krs"])
+    r1, W = R.cubic_circuit(cname)
+    assert oracle.g16_check(cname, r1, h("toxic"), h("wires"), h("r"), h("s"), ar, bs, krs) == 7
+
+
+@pytest.mark.parametrize("cname", ["bn254", "bls12377"])
+def test_oracle_setup_matches_pyref(oracle, cname):
+    """The C++ Setup restatement reproduces the pure-Python one (fixture pk)."""
+    g = _load("groth16_cubic_" + cname)
+    r1, W = R.cubic_circuit(cname)
+    pk = oracle.g16_setup(cname, r1, bytes.fromhex(g["toxic"]))
+    for k, v in g["pk"].items():
+        assert pk[k].tobytes().hex() == v, k
+
+
+# ---- C++ restatement vs pyref at random sizes -------------------------------------
+
+@pytest.mark.parametrize("cname", ["bn254", "bls12377"])
+def test_oracle_pippenger_vs_naive(oracle, cname):
+    c = pyref.CURVES[cname]
+    n = 300
+    sc = pyref.random_scalars(c, n, 5)
+    ks = R.encode_vec(cname, pyref.random_scalars(c, n, 6))
+    pts = oracle.batch_mul_base(cname, False, oracle.generator(cname, False), ks)
+    sb = R.encode_vec(cname, sc)
+    assert oracle.msm(cname, False, sb, pts) == oracle.msm(cname, False, sb, pts, naive=True)
+
+
+@pytest.mark.parametrize("cname", ["bn254", "bls12377"])
+def test_oracle_groth16_random_circuit(oracle, cname):
+    r1, W = R.squaring_chain(200, cname, x=7)
+    tox = R.encode_vec(cname, [11, 22, 33, 44, 55])
+    pk = oracle.g16_setup(cname, r1, tox)
+    a, b, cc = r1.solve_abc(W)
+    enc = lambda v: R.encode_vec(cname, v)
+    rb, sb = enc([3]), enc([4])
+    proof = oracle.g16_prove(cname, pk, r1.nb_public, enc(W), enc(a), enc(b), enc(cc), rb, sb)
+    assert oracle.g16_check(cname, r1, tox, enc(W), rb, sb, *proof) == 7
