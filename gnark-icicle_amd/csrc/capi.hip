@@ -27,40 +27,46 @@ GM_DEV uint64_t splitmix64(uint64_t& x) {
   return z ^ (z >> 31);
 }
 
+// n Montgomery (gnark-layout) scalars: random canonical value below 2^BITS,
+// reduced once (2^BITS < 2r for both scalar fields), then x*Rg.
 template <class Fr>
 __global__ void k_random_scalars(uint32_t* out, size_t n, uint64_t seed) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint64_t st = seed ^ (0xD1B54A32D192ED03ull * (i + 1));
-  Fe<Fr> k;
-  for (int q = 0; q < Fr::N / 2; q++) {
+  FeG<Fr> g;
+  for (int q = 0; q < Fr::NG / 2; q++) {
     uint64_t v = splitmix64(st);
-    k.v[2 * q] = (uint32_t)v;
-    k.v[2 * q + 1] = (uint32_t)(v >> 32);
+    g.w[2 * q] = (uint32_t)v;
+    g.w[2 * q + 1] = (uint32_t)(v >> 32);
   }
-  // clear bits above the modulus' top bit, then reduce once
-  const int top = Fr::BITS - 32 * (Fr::N - 1);
-  k.v[Fr::N - 1] &= (top >= 32) ? 0xffffffffu : ((1u << top) - 1);
+  const int top = Fr::BITS - 32 * (Fr::NG - 1);
+  g.w[Fr::NG - 1] &= (top >= 32) ? 0xffffffffu : ((1u << top) - 1);
+  Fe<Fr> k = fe_unpack<Fr>(g);
   fe_reduce_once(k);
-  k = fe_to_mont(k);
-  for (int q = 0; q < Fr::N; q++) out[i * Fr::N + q] = k.v[q];
+  feg_store<Fr>(out + i * Fr::NG, fe_pack(fe_canonical_to_gnark(k)));
 }
 
-// out[i] = [k_i] base (affine), double-and-add over the canonical scalar.
+// gnark-layout affine point passed by value
+template <class F>
+struct GPoint {
+  uint32_t w[2 * Coord<F>::WORDS];
+};
+
+// out[i] = [k_i] base (gnark-layout affine), double-and-add over the canonical scalar.
 template <class Fr, class F>
 __global__ void __launch_bounds__(128) k_batch_mul_base(const uint32_t* __restrict__ scalars,
-                                                        size_t n, Affine<F> base,
-                                                        Affine<F>* __restrict__ out) {
+                                                        size_t n, GPoint<F> base_g,
+                                                        uint32_t* __restrict__ out) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  Fe<Fr> k;
-  for (int q = 0; q < Fr::N; q++) k.v[q] = scalars[i * Fr::N + q];
-  k = fe_from_mont(k);
+  const FeG<Fr> k = fe_pack(fe_gnark_to_canonical(fe_load_g<Fr>(scalars, i)));
+  const Affine<F> base = load_affine_gnark<F>(base_g.w);
   XYZZ<F> acc = xyzz_inf<F>();
-  for (int w = Fr::N - 1; w >= 0; w--) {
+  for (int w = Fr::NG - 1; w >= 0; w--) {
     for (int b = 31; b >= 0; b--) {
       acc = xyzz_dbl(acc);
-      if ((k.v[w] >> b) & 1) xyzz_add_aff(acc, base);
+      if ((k.w[w] >> b) & 1) xyzz_add_aff(acc, base);
     }
   }
   Affine<F> r;
@@ -72,7 +78,7 @@ __global__ void __launch_bounds__(128) k_batch_mul_base(const uint32_t* __restri
     r.x = fe_mul(acc.x, fe_mul(t, acc.zzz));  // X / ZZ
     r.y = fe_mul(acc.y, fe_mul(t, acc.zz));   // Y / ZZZ
   }
-  out[i] = r;
+  store_affine_gnark<F>(out + i * 2 * Coord<F>::WORDS, r);
 }
 
 // dst[i] = src[idx[i]] (Fr, 32 bytes) -- device-side scalar compaction
@@ -413,10 +419,10 @@ extern "C++" {
 template <class C, bool G2>
 static int batch_mul_t(gm_ctx* ctx, const void* base, const void* sc, size_t n, void* out) {
   using DF = typename GroupSel<C, G2>::DF;
-  Affine<DF> b;
+  GPoint<DF> b;
   memcpy(&b, base, sizeof(b));
   hipLaunchKernelGGL((k_batch_mul_base<typename C::Fr, DF>), dim3(blocks_for(n, 128)), dim3(128), 0,
-                     ctx->stream, (const uint32_t*)sc, n, b, (Affine<DF>*)out);
+                     ctx->stream, (const uint32_t*)sc, n, b, (uint32_t*)out);
   GM_HIP(hipGetLastError());
   GM_HIP(hipStreamSynchronize(ctx->stream));
   return GM_OK;
@@ -466,9 +472,34 @@ int gm_g16_pk_upload(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, gm_g16_pk*
     return GM_OK;
   };
   int rc;
-  if ((rc = up(h->g1_A, g1b * pk->nbA, &pk->A)) || (rc = up(h->g1_B, g1b * pk->nbB, &pk->B)) ||
-      (rc = up(h->g1_Z, g1b * (pk->n - 1), &pk->Z)) || (rc = up(h->g1_K, g1b * pk->nbK, &pk->K)) ||
-      (rc = up(h->g2_B, g2b * pk->nbB, &pk->B2))) {
+  // upload gnark-layout points, convert once into the device-internal layout
+  // (radix-2^29 Montgomery) the MSM kernels consume (setupDevicePointers).
+  auto up_pts = [&](const void* src, size_t count, bool g2, void** dst) -> int {
+    void* tmp = nullptr;
+    int r = up(src, (g2 ? g2b : g1b) * count, &tmp);
+    if (r) return r;
+    size_t ib = 0;
+    if (curve == GM_BN254) ib = g2 ? msm_internal_point_bytes<CurveBN254, true>() : msm_internal_point_bytes<CurveBN254, false>();
+    else ib = g2 ? msm_internal_point_bytes<CurveBLS12377, true>() : msm_internal_point_bytes<CurveBLS12377, false>();
+    hipError_t e = hipMalloc(dst, ib * (count ? count : 1));
+    if (e != hipSuccess) {
+      hipFree(tmp);
+      set_error(std::string("pk upload hipMalloc: ") + hipGetErrorString(e));
+      return GM_ERR_OOM;
+    }
+    if (curve == GM_BN254)
+      r = g2 ? msm_prepare_points<CurveBN254, true>(ctx, tmp, count, *dst)
+             : msm_prepare_points<CurveBN254, false>(ctx, tmp, count, *dst);
+    else
+      r = g2 ? msm_prepare_points<CurveBLS12377, true>(ctx, tmp, count, *dst)
+             : msm_prepare_points<CurveBLS12377, false>(ctx, tmp, count, *dst);
+    hipStreamSynchronize(ctx->stream);
+    hipFree(tmp);
+    return r;
+  };
+  if ((rc = up_pts(h->g1_A, pk->nbA, false, &pk->A)) || (rc = up_pts(h->g1_B, pk->nbB, false, &pk->B)) ||
+      (rc = up_pts(h->g1_Z, pk->n - 1, false, &pk->Z)) || (rc = up_pts(h->g1_K, pk->nbK, false, &pk->K)) ||
+      (rc = up_pts(h->g2_B, pk->nbB, true, &pk->B2))) {
     delete pk;
     return rc;
   }
@@ -557,21 +588,21 @@ static int g16_prove_t(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, void* 
   J1 d0 = host::jmul(dj, rc_.v, 4), d1 = host::jmul(dj, sc_.v, 4), d2 = host::jmul(dj, krc.v, 4);
   HF1 t1[3];
   // Ar = MSM(wA, A) + alpha + r delta   (computeAR1 icicle.go:312-324)
-  if ((rc = msm_device<C, false>(ctx, wA.p, pk->A, pk->nbA, t1))) return rc;
+  if ((rc = msm_device<C, false>(ctx, wA.p, pk->A, pk->nbA, t1, true))) return rc;
   J1 ar = host::jadd(host::jadd_aff(J1{t1[0], t1[1], t1[2]}, alpha), d0);
   // Bs1 = MSM(wB, B) + beta + s delta   (computeBS1 icicle.go:299-310)
-  if ((rc = msm_device<C, false>(ctx, wB.p, pk->B, pk->nbB, t1))) return rc;
+  if ((rc = msm_device<C, false>(ctx, wB.p, pk->B, pk->nbB, t1, true))) return rc;
   J1 bs1 = host::jadd(host::jadd_aff(J1{t1[0], t1[1], t1[2]}, beta), d1);
   // Krs = MSM(wK, K) + kr delta + MSM(h[:n-1], Z) + s Ar + r Bs1   (computeKRS icicle.go:326-375)
-  if ((rc = msm_device<C, false>(ctx, wK.p, pk->K, pk->nbK, t1))) return rc;
+  if ((rc = msm_device<C, false>(ctx, wK.p, pk->K, pk->nbK, t1, true))) return rc;
   J1 krs = host::jadd(J1{t1[0], t1[1], t1[2]}, d2);
-  if ((rc = msm_device<C, false>(ctx, a, pk->Z, n - 1, t1))) return rc;
+  if ((rc = msm_device<C, false>(ctx, a, pk->Z, n - 1, t1, true))) return rc;
   krs = host::jadd(krs, J1{t1[0], t1[1], t1[2]});
   krs = host::jadd(krs, host::jmul(ar, sc_.v, 4));
   krs = host::jadd(krs, host::jmul(bs1, rc_.v, 4));
   // Bs = MSM_G2(wB, B2) + s delta2 + beta2   (computeBS2 icicle.go:377-393)
   HF2 t2[3];
-  if ((rc = msm_device<C, true>(ctx, wB.p, pk->B2, pk->nbB, t2))) return rc;
+  if ((rc = msm_device<C, true>(ctx, wB.p, pk->B2, pk->nbB, t2, true))) return rc;
   host::Aff<HF2> beta2, delta2;
   memcpy(&beta2, pk->beta2.data(), sizeof(beta2));
   memcpy(&delta2, pk->delta2.data(), sizeof(delta2));

@@ -153,6 +153,20 @@ GM_DEV XYZZ<F> xyzz_add(const XYZZ<F>& a, const XYZZ<F>& b) {
   return r;
 }
 
+// Affine point in gnark layout (X then Y, each Coord<F>::WORDS u32) -> internal.
+template <class F>
+GM_DEV Affine<F> load_affine_gnark(const uint32_t* __restrict__ src) {
+  Affine<F> r;
+  r.x = Coord<F>::load_internal(src);
+  r.y = Coord<F>::load_internal(src + Coord<F>::WORDS);
+  return r;
+}
+template <class F>
+GM_DEV void store_affine_gnark(uint32_t* __restrict__ dst, const Affine<F>& a) {
+  Coord<F>::store_gnark(dst, a.x);
+  Coord<F>::store_gnark(dst + Coord<F>::WORDS, a.y);
+}
+
 template <class F>
 GM_DEV Affine<F> aff_neg(const Affine<F>& p) {
   Affine<F> r;

@@ -1,14 +1,26 @@
 // Device-side prime-field arithmetic for the MSM / NTT hot path (gfx950).
 //
-// Layout contract (SURVEY.md §8 preamble): elements are stored exactly as
-// gnark-crypto stores fp.Element / fr.Element -- little-endian 64-bit limbs in
-// Montgomery form x*R mod p with R = 2^(64*limbs).  Read as 32-bit words the
-// same bytes are little-endian u32 limbs with the same R, so the kernels consume
-// gnark's raw memory with zero conversion.
+// Two representations of an element x of F_p:
 //
-// Arithmetic is 32-bit-limb CIOS Montgomery multiplication built on
-// v_mad_u64_u32.  All moduli here have a spare top bit (msw < 2^31 - 1), which
-// allows the "no-carry" CIOS variant (no (N+1)-th accumulator word).
+//  * gnark layout (HBM, C-ABI): exactly gnark-crypto's fp.Element / fr.Element --
+//    little-endian 64-bit limbs in Montgomery form x*Rg mod p, Rg = 2^(64*limbs).
+//    Read as NG little-endian u32 words.  Points, scalars and NTT vectors cross
+//    the boundary in this form, byte for byte.
+//
+//  * internal (registers / LDS / device scratch): N unsaturated 29-bit limbs
+//    (radix 2^29, one limb per u32) in Montgomery form x*R' mod p,
+//    R' = 2^(29N) (N = 9 for the 254/253-bit fields, 14 for BLS12-377 Fp).
+//    Values are kept canonical (< p, every limb < 2^29).
+//
+// Why radix 2^29: a finely-integrated product-scanning Montgomery product then
+// accumulates every column (<= 2N products of 58 bits) in one 64-bit register
+// with v_mad_u64_u32 and no carry flags at all -- no VALU->VCC carry chains
+// (which need 2 hazard wait states each on gfx950) and no 32-bit carry-word
+// shuffling.  Measured 147-159 Gmul/s vs 87-96 for 32-bit CIOS on MI355X
+// (tools/microbench/mul29.hip).
+//
+// Mixed-form identity used by the NTT: mul(a_gnark, w_internal) = a*w in gnark
+// form (x*Rg * w*R' / R' = (x*w)*Rg), so NTT data never needs converting.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -19,42 +31,44 @@ namespace gm {
 #define GM_DEV __device__ __forceinline__
 #define GM_HD __host__ __device__ __forceinline__
 
-// ---------------------------------------------------------------------------
-// Field descriptors: N u32 limbs + constants returned by constexpr accessors so
-// that fully-unrolled loops fold every modulus word into an instruction literal.
-// ---------------------------------------------------------------------------
-#define GM_DEFINE_FIELD(NAME, TAG, NLIMBS)                                        \
-  struct NAME {                                                                   \
-    static constexpr int N = NLIMBS;                                              \
-    static constexpr int BITS = GM_##TAG##_BITS;                                  \
-    static constexpr uint32_t INV = GM_##TAG##_INV32;                             \
-    GM_HD static constexpr uint32_t p(int i) {                                    \
-      constexpr uint32_t a[NLIMBS] = GM_##TAG##_P32;                              \
-      return a[i];                                                                \
-    }                                                                             \
-    GM_HD static constexpr uint32_t one(int i) {                                  \
-      constexpr uint32_t a[NLIMBS] = GM_##TAG##_ONE32;                            \
-      return a[i];                                                                \
-    }                                                                             \
-    GM_HD static constexpr uint32_t r2(int i) {                                   \
-      constexpr uint32_t a[NLIMBS] = GM_##TAG##_R2_32;                            \
-      return a[i];                                                                \
-    }                                                                             \
-    /* limbs of p - 2 (Fermat exponent), borrow propagated */                     \
-    GM_HD static constexpr uint32_t pm2(int i) {                                  \
-      uint64_t borrow = 2;                                                        \
-      for (int k = 0;; k++) {                                                     \
-        const uint64_t v = (uint64_t)p(k) - borrow;                               \
-        if (k == i) return (uint32_t)v;                                           \
-        borrow = (v >> 63) & 1;                                                   \
-      }                                                                           \
-    }                                                                             \
+constexpr int RADIX = 29;
+constexpr uint32_t LIMB_MASK = (1u << RADIX) - 1;
+
+#define GM_CONST_ARRAY_FN(FN, N, INIT)       \
+  GM_HD static constexpr uint32_t FN(int i) { \
+    constexpr uint32_t a[N] = INIT;           \
+    return a[i];                              \
+  }
+
+#define GM_DEFINE_FIELD(NAME, TAG)                                              \
+  struct NAME {                                                                 \
+    static constexpr int N = GM_##TAG##_N29;  /* radix-2^29 limbs */            \
+    static constexpr int NG = GM_##TAG##_NG;  /* gnark u32 words */             \
+    static constexpr int BITS = GM_##TAG##_BITS;                                \
+    static constexpr uint32_t INV = GM_##TAG##_INV29;                           \
+    GM_CONST_ARRAY_FN(p, GM_##TAG##_N29, GM_##TAG##_P29)                        \
+    GM_CONST_ARRAY_FN(one, GM_##TAG##_N29, GM_##TAG##_ONE29)                    \
+    GM_CONST_ARRAY_FN(r2, GM_##TAG##_N29, GM_##TAG##_R229)                      \
+    GM_CONST_ARRAY_FN(kin, GM_##TAG##_N29, GM_##TAG##_KIN29)                    \
+    GM_CONST_ARRAY_FN(kout, GM_##TAG##_N29, GM_##TAG##_KOUT29)                  \
+    GM_CONST_ARRAY_FN(kcan, GM_##TAG##_N29, GM_##TAG##_KCAN29)                  \
+    GM_CONST_ARRAY_FN(kgn, GM_##TAG##_N29, GM_##TAG##_KGN29)                    \
+    GM_CONST_ARRAY_FN(pg, GM_##TAG##_NG, GM_##TAG##_P32)                        \
+    /* u32 words of p - 2 (Fermat exponent), borrow propagated */               \
+    GM_HD static constexpr uint32_t pm2(int i) {                                \
+      uint64_t borrow = 2;                                                      \
+      for (int k = 0;; k++) {                                                   \
+        const uint64_t v = (uint64_t)pg(k) - borrow;                            \
+        if (k == i) return (uint32_t)v;                                         \
+        borrow = (v >> 63) & 1;                                                 \
+      }                                                                         \
+    }                                                                           \
   };
 
-GM_DEFINE_FIELD(Bn254Fp, BN254_FP, 8)
-GM_DEFINE_FIELD(Bn254Fr, BN254_FR, 8)
-GM_DEFINE_FIELD(Bls377Fp, BLS12377_FP, 12)
-GM_DEFINE_FIELD(Bls377Fr, BLS12377_FR, 8)
+GM_DEFINE_FIELD(Bn254Fp, BN254_FP)
+GM_DEFINE_FIELD(Bn254Fr, BN254_FR)
+GM_DEFINE_FIELD(Bls377Fp, BLS12377_FP)
+GM_DEFINE_FIELD(Bls377Fr, BLS12377_FR)
 
 template <class P>
 struct Fe {
@@ -62,17 +76,18 @@ struct Fe {
   uint32_t v[P::N];
 };
 
-// --- carry helpers -----------------------------------------------------------
-GM_DEV uint32_t add_cc(uint32_t a, uint32_t b, uint32_t& carry) {
-  uint64_t s = (uint64_t)a + b + carry;
-  carry = (uint32_t)(s >> 32);
-  return (uint32_t)s;
-}
-GM_DEV uint32_t sub_bb(uint32_t a, uint32_t b, uint32_t& borrow) {
-  uint64_t d = (uint64_t)a - b - borrow;
-  borrow = (uint32_t)(d >> 63);
-  return (uint32_t)d;
-}
+// Packed gnark-layout words of one element (NG u32).
+template <class P>
+struct FeG {
+  uint32_t w[P::NG];
+};
+
+#define GM_FE_CONST(P, FN)                                                    \
+  ([]() {                                                                     \
+    ::gm::Fe<P> r_;                                                           \
+    _Pragma("unroll") for (int i_ = 0; i_ < P::N; i_++) r_.v[i_] = P::FN(i_); \
+    return r_;                                                                \
+  }())
 
 template <class P>
 GM_DEV Fe<P> fe_zero() {
@@ -103,16 +118,99 @@ GM_DEV bool fe_eq(const Fe<P>& a, const Fe<P>& b) {
   return acc == 0;
 }
 
-// r = a - p if a >= p  (a < 2p)
+// ---------------------------------------------------------------------------
+// pack / unpack between NG x u32 (gnark words) and N x 29-bit limbs (same
+// integer; no field conversion).  Fully unrolled bit plumbing.
+// ---------------------------------------------------------------------------
+template <class P>
+GM_DEV Fe<P> fe_unpack(const FeG<P>& g) {
+  Fe<P> r;
+#pragma unroll
+  for (int i = 0; i < P::N; i++) {
+    const int bit = RADIX * i, w = bit >> 5, s = bit & 31;
+    const uint32_t lo = (w < P::NG) ? g.w[w] : 0u;
+    const uint32_t hi = (w + 1 < P::NG) ? g.w[w + 1] : 0u;
+    const uint64_t x = ((uint64_t)hi << 32) | lo;
+    r.v[i] = (uint32_t)(x >> s) & LIMB_MASK;
+  }
+  return r;
+}
+template <class P>
+GM_DEV FeG<P> fe_pack(const Fe<P>& a) {
+  FeG<P> g;
+#pragma unroll
+  for (int j = 0; j < P::NG; j++) {
+    const int bit = 32 * j, i0 = bit / RADIX, s0 = bit % RADIX;
+    uint64_t x = 0;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const int i = i0 + k;
+      if (i < P::N) {
+        const int sh = RADIX * k - s0;
+        if (sh >= 0) x |= (uint64_t)a.v[i] << sh;
+        else x |= (uint64_t)a.v[i] >> (-sh);
+      }
+    }
+    g.w[j] = (uint32_t)x;
+  }
+  return g;
+}
+
+// vectorised loads / stores of gnark words (16 B, then an 8 B tail)
+template <class P>
+GM_DEV FeG<P> feg_load(const uint32_t* __restrict__ src) {
+  FeG<P> g;
+  static_assert(P::NG % 2 == 0, "gnark elements are whole u64 limbs");
+#pragma unroll
+  for (int q = 0; q < P::NG / 4; q++) {
+    const uint4 v = reinterpret_cast<const uint4*>(src)[q];
+    g.w[4 * q] = v.x;
+    g.w[4 * q + 1] = v.y;
+    g.w[4 * q + 2] = v.z;
+    g.w[4 * q + 3] = v.w;
+  }
+  if constexpr (P::NG % 4 != 0) {
+    const uint2 v = reinterpret_cast<const uint2*>(src)[P::NG / 2 - 1];
+    g.w[P::NG - 2] = v.x;
+    g.w[P::NG - 1] = v.y;
+  }
+  return g;
+}
+template <class P>
+GM_DEV void feg_store(uint32_t* __restrict__ dst, const FeG<P>& g) {
+#pragma unroll
+  for (int q = 0; q < P::NG / 4; q++)
+    reinterpret_cast<uint4*>(dst)[q] = make_uint4(g.w[4 * q], g.w[4 * q + 1], g.w[4 * q + 2], g.w[4 * q + 3]);
+  if constexpr (P::NG % 4 != 0)
+    reinterpret_cast<uint2*>(dst)[P::NG / 2 - 1] = make_uint2(g.w[P::NG - 2], g.w[P::NG - 1]);
+}
+// element idx of a gnark-layout array: unpacked, still in gnark form
+template <class P>
+GM_DEV Fe<P> fe_load_g(const void* base, size_t idx) {
+  return fe_unpack<P>(feg_load<P>(reinterpret_cast<const uint32_t*>(base) + idx * P::NG));
+}
+template <class P>
+GM_DEV void fe_store_g(void* base, size_t idx, const Fe<P>& a) {
+  feg_store<P>(reinterpret_cast<uint32_t*>(base) + idx * P::NG, fe_pack(a));
+}
+
+// ---------------------------------------------------------------------------
+// arithmetic on canonical internal elements
+// ---------------------------------------------------------------------------
+// a - p if a >= p (a < 2p, limbs < 2^29)
 template <class P>
 GM_DEV void fe_reduce_once(Fe<P>& a) {
   Fe<P> t;
-  uint32_t borrow = 0;
+  int32_t borrow = 0;
 #pragma unroll
-  for (int i = 0; i < P::N; i++) t.v[i] = sub_bb(a.v[i], P::p(i), borrow);
-  // borrow == 0  <=> a >= p  -> take t
+  for (int i = 0; i < P::N; i++) {
+    const int32_t d = (int32_t)a.v[i] - (int32_t)P::p(i) + borrow;
+    borrow = d >> RADIX;  // 0 or -1
+    t.v[i] = (uint32_t)d & LIMB_MASK;
+  }
+  const bool ge = borrow == 0;
 #pragma unroll
-  for (int i = 0; i < P::N; i++) a.v[i] = borrow ? a.v[i] : t.v[i];
+  for (int i = 0; i < P::N; i++) a.v[i] = ge ? t.v[i] : a.v[i];
 }
 
 template <class P>
@@ -120,22 +218,34 @@ GM_DEV Fe<P> fe_add(const Fe<P>& a, const Fe<P>& b) {
   Fe<P> r;
   uint32_t c = 0;
 #pragma unroll
-  for (int i = 0; i < P::N; i++) r.v[i] = add_cc(a.v[i], b.v[i], c);
-  fe_reduce_once(r);  // spare top bit: a+b < 2p < 2^(32N), no overflow word
+  for (int i = 0; i < P::N; i++) {
+    const uint32_t s = a.v[i] + b.v[i] + c;
+    r.v[i] = s & LIMB_MASK;
+    c = s >> RADIX;
+  }
+  fe_reduce_once(r);  // a + b < 2p < R'
   return r;
 }
 
 template <class P>
 GM_DEV Fe<P> fe_sub(const Fe<P>& a, const Fe<P>& b) {
   Fe<P> r;
-  uint32_t borrow = 0;
+  int32_t borrow = 0;
 #pragma unroll
-  for (int i = 0; i < P::N; i++) r.v[i] = sub_bb(a.v[i], b.v[i], borrow);
-  // if borrow, add p back
-  uint32_t mask = 0u - borrow;
+  for (int i = 0; i < P::N; i++) {
+    const int32_t d = (int32_t)a.v[i] - (int32_t)b.v[i] + borrow;
+    borrow = d >> RADIX;
+    r.v[i] = (uint32_t)d & LIMB_MASK;
+  }
+  // negative -> add p back
+  const uint32_t msk = (uint32_t)borrow;  // 0 or 0xffffffff
   uint32_t c = 0;
 #pragma unroll
-  for (int i = 0; i < P::N; i++) r.v[i] = add_cc(r.v[i], P::p(i) & mask, c);
+  for (int i = 0; i < P::N; i++) {
+    const uint32_t s = r.v[i] + (P::p(i) & msk) + c;
+    r.v[i] = s & LIMB_MASK;
+    c = s >> RADIX;
+  }
   return r;
 }
 
@@ -146,130 +256,96 @@ GM_DEV Fe<P> fe_dbl(const Fe<P>& a) {
 
 template <class P>
 GM_DEV Fe<P> fe_neg(const Fe<P>& a) {
-  Fe<P> r;
-  uint32_t borrow = 0;
-#pragma unroll
-  for (int i = 0; i < P::N; i++) r.v[i] = sub_bb(P::p(i), a.v[i], borrow);
-  const bool z = fe_is_zero(a);
-#pragma unroll
-  for (int i = 0; i < P::N; i++) r.v[i] = z ? 0u : r.v[i];
-  return r;
+  return fe_sub(fe_zero<P>(), a);
 }
 
-// CIOS Montgomery multiplication, no-carry variant (requires p.msw < 2^31-1).
-// Plain C: the compiler owns every carry and inserts the gfx950 VALU->carry
-// hazard padding itself.
+// Finely-integrated product-scanning Montgomery product in radix 2^29:
+// column k accumulates a_i b_{k-i} + m_i p_{k-i} (< 2N * 2^58 < 2^64) in one
+// 64-bit register; m_k = (acc * (-p^-1)) mod 2^29 zeroes the low limb.
+// Inputs < p  ->  result < 2p -> one conditional subtraction -> canonical.
 template <class P>
 GM_DEV Fe<P> fe_mul(const Fe<P>& a, const Fe<P>& b) {
-  constexpr int N = P::N;
-  uint32_t t[N];
-#pragma unroll
-  for (int j = 0; j < N; j++) t[j] = 0;
-#pragma unroll
-  for (int i = 0; i < N; i++) {
-    uint64_t acc = (uint64_t)a.v[0] * b.v[i] + t[0];
-    t[0] = (uint32_t)acc;
-    uint32_t C = (uint32_t)(acc >> 32);
-#pragma unroll
-    for (int j = 1; j < N; j++) {
-      acc = (uint64_t)a.v[j] * b.v[i] + t[j] + C;
-      t[j] = (uint32_t)acc;
-      C = (uint32_t)(acc >> 32);
-    }
-    const uint32_t A = C;
-    const uint32_t m = t[0] * P::INV;
-    acc = (uint64_t)m * P::p(0) + t[0];
-    C = (uint32_t)(acc >> 32);
-#pragma unroll
-    for (int j = 1; j < N; j++) {
-      acc = (uint64_t)m * P::p(j) + t[j] + C;
-      t[j - 1] = (uint32_t)acc;
-      C = (uint32_t)(acc >> 32);
-    }
-    t[N - 1] = C + A;
-  }
-  Fe<P> r;
-#pragma unroll
-  for (int j = 0; j < N; j++) r.v[j] = t[j];
-  fe_reduce_once(r);
-  return r;
-}
-
-// acc(64) += a*b with the carry out of the 64-bit accumulator added to hi.
-// v_mad_u64_u32 reports that carry in an SGPR pair; v_addc_co_u32 folds it in.
-GM_DEV void mad_acc(uint32_t a, uint32_t b, uint64_t& acc, uint32_t& hi) {
-  uint64_t c;
-  asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(c) : "v"(a), "v"(b));
-  asm("v_addc_co_u32 %0, %1, %2, 0, %3" : "=v"(hi), "=s"(c) : "v"(hi), "s"(c));
-}
-GM_DEV void mad_acc_s(uint32_t a, uint32_t b_uniform, uint64_t& acc, uint32_t& hi) {
-  uint64_t c;
-  asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(c) : "v"(a), "s"(b_uniform));
-  asm("v_addc_co_u32 %0, %1, %2, 0, %3" : "=v"(hi), "=s"(c) : "v"(hi), "s"(c));
-}
-
-// Finely-integrated product-scanning (FIPS) Montgomery multiplication:
-// column k accumulates a_i*b_{k-i} and m_i*p_{k-i} into a 64-bit accumulator
-// plus a carry word; 2N^2 v_mad_u64_u32 and no per-row carry propagation.
-// EXPERIMENTAL / NOT USED: the carry hand-off between the two asm statements
-// is a VALU-SGPR-write -> VALU-carry-read hazard that needs 2 wait states on
-// gfx950, but hipcc only pads 1 around inline asm -> intermittent stale
-// carries.  Kept for the microbenchmark until a hazard-safe form exists.
-template <class P>
-GM_DEV Fe<P> fe_mul_fips_asm(const Fe<P>& a, const Fe<P>& b) {
   constexpr int N = P::N;
   uint32_t m[N];
   Fe<P> r;
   uint64_t acc = 0;
 #pragma unroll
   for (int k = 0; k < 2 * N - 1; k++) {
-    uint32_t hi = 0;
 #pragma unroll
     for (int i = (k - N + 1 > 0 ? k - N + 1 : 0); i <= (k < N - 1 ? k : N - 1); i++)
-      mad_acc(a.v[i], b.v[k - i], acc, hi);
+      acc += (uint64_t)a.v[i] * b.v[k - i];
 #pragma unroll
     for (int i = (k - N + 1 > 0 ? k - N + 1 : 0); i <= (k - 1 < N - 1 ? k - 1 : N - 1); i++)
-      mad_acc_s(m[i], P::p(k - i), acc, hi);
+      acc += (uint64_t)m[i] * P::p(k - i);
     if (k < N) {
-      m[k] = (uint32_t)acc * P::INV;
-      mad_acc_s(m[k], P::p(0), acc, hi);
+      m[k] = ((uint32_t)acc * P::INV) & LIMB_MASK;
+      acc += (uint64_t)m[k] * P::p(0);
     } else {
-      r.v[k - N] = (uint32_t)acc;
+      r.v[k - N] = (uint32_t)acc & LIMB_MASK;
     }
-    acc = (acc >> 32) | ((uint64_t)hi << 32);
+    acc >>= RADIX;
   }
   r.v[N - 1] = (uint32_t)acc;
   fe_reduce_once(r);
   return r;
 }
 
+// Squaring: the symmetric products a_i a_j (i != j) are formed once and doubled.
 template <class P>
 GM_DEV Fe<P> fe_sqr(const Fe<P>& a) {
-  return fe_mul(a, a);
+  constexpr int N = P::N;
+  uint32_t m[N];
+  Fe<P> r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * N - 1; k++) {
+    uint64_t cross = 0;
+#pragma unroll
+    for (int i = (k - N + 1 > 0 ? k - N + 1 : 0); i <= (k < N - 1 ? k : N - 1); i++) {
+      const int j = k - i;
+      if (i < j) cross += (uint64_t)a.v[i] * a.v[j];
+    }
+    acc += cross << 1;
+    if ((k & 1) == 0) acc += (uint64_t)a.v[k / 2] * a.v[k / 2];
+#pragma unroll
+    for (int i = (k - N + 1 > 0 ? k - N + 1 : 0); i <= (k - 1 < N - 1 ? k - 1 : N - 1); i++)
+      acc += (uint64_t)m[i] * P::p(k - i);
+    if (k < N) {
+      m[k] = ((uint32_t)acc * P::INV) & LIMB_MASK;
+      acc += (uint64_t)m[k] * P::p(0);
+    } else {
+      r.v[k - N] = (uint32_t)acc & LIMB_MASK;
+    }
+    acc >>= RADIX;
+  }
+  r.v[N - 1] = (uint32_t)acc;
+  fe_reduce_once(r);
+  return r;
 }
 
-// Montgomery -> canonical integer (multiply by 1).
+// form conversions (see header comment)
 template <class P>
-GM_DEV Fe<P> fe_from_mont(const Fe<P>& a) {
-  Fe<P> one;
-#pragma unroll
-  for (int i = 0; i < P::N; i++) one.v[i] = (i == 0);
-  return fe_mul(a, one);
-}
-// canonical -> Montgomery (multiply by R^2).
+GM_DEV Fe<P> fe_to_internal(const Fe<P>& gnark_form) { return fe_mul(gnark_form, GM_FE_CONST(P, kin)); }
 template <class P>
-GM_DEV Fe<P> fe_to_mont(const Fe<P>& a) {
-  Fe<P> r2;
-#pragma unroll
-  for (int i = 0; i < P::N; i++) r2.v[i] = P::r2(i);
-  return fe_mul(a, r2);
+GM_DEV Fe<P> fe_to_gnark(const Fe<P>& internal) { return fe_mul(internal, GM_FE_CONST(P, kout)); }
+template <class P>
+GM_DEV Fe<P> fe_gnark_to_canonical(const Fe<P>& gnark_form) { return fe_mul(gnark_form, GM_FE_CONST(P, kcan)); }
+template <class P>
+GM_DEV Fe<P> fe_canonical_to_gnark(const Fe<P>& x) { return fe_mul(x, GM_FE_CONST(P, kgn)); }
+template <class P>
+GM_DEV Fe<P> fe_to_mont(const Fe<P>& x) { return fe_mul(x, GM_FE_CONST(P, r2)); }
+template <class P>
+GM_DEV Fe<P> fe_from_mont(const Fe<P>& internal) {
+  Fe<P> o = fe_zero<P>();
+  o.v[0] = 1;
+  return fe_mul(internal, o);
 }
 
-// a^(p-2) (Fermat inversion; 0 -> 0).
+// a^(p-2) (Fermat inversion; 0 -> 0), internal form in and out.
 template <class P>
 GM_DEV Fe<P> fe_inv(const Fe<P>& a) {
   Fe<P> r = fe_one<P>();
-  for (int i = P::N - 1; i >= 0; i--) {
+  for (int i = P::NG - 1; i >= 0; i--) {
     const uint32_t e = P::pm2(i);
     for (int b = 31; b >= 0; b--) {
       r = fe_sqr(r);
@@ -334,15 +410,14 @@ GM_DEV Fe2<P, BETA> fe_mul(const Fe2<P, BETA>& a, const Fe2<P, BETA>& b) {
 template <class P, int BETA>
 GM_DEV Fe2<P, BETA> fe_sqr(const Fe2<P, BETA>& a) {
   // (a0 + a1 u)^2 = a0^2 + BETA a1^2 + 2 a0 a1 u
-  Fe<P> v0 = fe_mul(a.a0, a.a0);
-  Fe<P> v1 = fe_mul(a.a1, a.a1);
+  Fe<P> v0 = fe_sqr(a.a0);
+  Fe<P> v1 = fe_sqr(a.a1);
   Fe<P> c = fe_mul(a.a0, a.a1);
   Fe2<P, BETA> r;
   r.a0 = fe_add(v0, mul_by_beta<P, BETA>(v1));
   r.a1 = fe_dbl(c);
   return r;
 }
-
 template <class P, int BETA>
 GM_DEV Fe2<P, BETA> fe_inv(const Fe2<P, BETA>& a) {
   // 1/(a0 + a1 u) = (a0 - a1 u) / (a0^2 - BETA a1^2)
@@ -350,5 +425,26 @@ GM_DEV Fe2<P, BETA> fe_inv(const Fe2<P, BETA>& a) {
   Fe<P> ni = fe_inv(nrm);
   return {fe_mul(a.a0, ni), fe_neg(fe_mul(a.a1, ni))};
 }
+
+// gnark-layout <-> internal for a coordinate field (Fe or Fe2).
+template <class F>
+struct Coord;
+template <class P>
+struct Coord<Fe<P>> {
+  static constexpr int WORDS = P::NG;  // u32 words in gnark layout
+  GM_DEV static Fe<P> load_internal(const uint32_t* src) { return fe_to_internal(fe_unpack<P>(feg_load<P>(src))); }
+  GM_DEV static void store_gnark(uint32_t* dst, const Fe<P>& a) { feg_store<P>(dst, fe_pack(fe_to_gnark(a))); }
+};
+template <class P, int B>
+struct Coord<Fe2<P, B>> {
+  static constexpr int WORDS = 2 * P::NG;
+  GM_DEV static Fe2<P, B> load_internal(const uint32_t* src) {
+    return {Coord<Fe<P>>::load_internal(src), Coord<Fe<P>>::load_internal(src + P::NG)};
+  }
+  GM_DEV static void store_gnark(uint32_t* dst, const Fe2<P, B>& a) {
+    Coord<Fe<P>>::store_gnark(dst, a.a0);
+    Coord<Fe<P>>::store_gnark(dst + P::NG, a.a1);
+  }
+};
 
 }  // namespace gm

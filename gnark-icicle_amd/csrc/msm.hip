@@ -18,7 +18,6 @@
 // Exact group arithmetic: the result is independent of summation order, so the
 // atomics-based counting sort needs no determinism.
 #include <hipcub/hipcub.hpp>
-#include <cstdlib>
 
 #include "curves.hpp"
 #include "msm.hpp"
@@ -30,31 +29,22 @@ namespace gm {
 // scalar digits
 // ---------------------------------------------------------------------------
 template <class Fr>
-GM_DEV uint32_t window_bits(const Fe<Fr>& k, uint32_t bit, uint32_t mask) {
+GM_DEV uint32_t window_bits(const FeG<Fr>& k, uint32_t bit, uint32_t mask) {
   const uint32_t idx = bit >> 5, sh = bit & 31;
   uint32_t lo = 0, hi = 0;
 #pragma unroll
-  for (int i = 0; i < Fr::N; i++) {
-    lo = (idx == (uint32_t)i) ? k.v[i] : lo;
-    hi = (idx + 1 == (uint32_t)i) ? k.v[i] : hi;
+  for (int i = 0; i < Fr::NG; i++) {
+    lo = (idx == (uint32_t)i) ? k.w[i] : lo;
+    hi = (idx + 1 == (uint32_t)i) ? k.w[i] : hi;
   }
   const uint64_t v = ((uint64_t)hi << 32) | lo;
   return (uint32_t)(v >> sh) & mask;
 }
 
+// gnark Montgomery fr.Element -> canonical integer as packed u32 words
 template <class Fr>
-GM_DEV Fe<Fr> load_scalar_canonical(const uint32_t* __restrict__ s, uint32_t i) {
-  Fe<Fr> k;
-  const uint4* p = reinterpret_cast<const uint4*>(s + (size_t)i * Fr::N);
-#pragma unroll
-  for (int q = 0; q < Fr::N / 4; q++) {
-    uint4 v = p[q];
-    k.v[4 * q + 0] = v.x;
-    k.v[4 * q + 1] = v.y;
-    k.v[4 * q + 2] = v.z;
-    k.v[4 * q + 3] = v.w;
-  }
-  return fe_from_mont(k);
+GM_DEV FeG<Fr> load_scalar_canonical(const uint32_t* __restrict__ s, uint32_t i) {
+  return fe_pack(fe_gnark_to_canonical(fe_load_g<Fr>(s, i)));
 }
 
 // Signed digit recoding: raw = bits + carry; raw > 2^(c-1) -> digit raw - 2^c.
@@ -65,7 +55,7 @@ __global__ void __launch_bounds__(256) k_msm_hist(const uint32_t* __restrict__ s
                                                   uint32_t* __restrict__ counts) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const Fe<Fr> k = load_scalar_canonical<Fr>(scalars, i);
+  const FeG<Fr> k = load_scalar_canonical<Fr>(scalars, i);
   const uint32_t nb = 1u << (c - 1), mask = (1u << c) - 1;
   uint32_t carry = 0;
   for (uint32_t w = 0; w < W; w++) {
@@ -91,7 +81,7 @@ __global__ void __launch_bounds__(256) k_msm_scatter(const uint32_t* __restrict_
                                                      uint32_t* __restrict__ err) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const Fe<Fr> k = load_scalar_canonical<Fr>(scalars, i);
+  const FeG<Fr> k = load_scalar_canonical<Fr>(scalars, i);
   const uint32_t nb = 1u << (c - 1), mask = (1u << c) - 1;
   uint32_t carry = 0;
   for (uint32_t w = 0; w < W; w++) {
@@ -118,18 +108,14 @@ __global__ void __launch_bounds__(256) k_msm_scatter(const uint32_t* __restrict_
 }
 
 // ---------------------------------------------------------------------------
-// point loads (gnark affine layout, 16-byte vector loads)
+// points: gnark layout -> internal layout (once per MSM, into workspace)
 // ---------------------------------------------------------------------------
 template <class F>
-GM_DEV Affine<F> load_affine(const Affine<F>* __restrict__ pts, uint32_t idx) {
-  static_assert(sizeof(Affine<F>) % 16 == 0, "affine point must be 16B multiple");
-  constexpr int Q = sizeof(Affine<F>) / 16;
-  const uint4* src = reinterpret_cast<const uint4*>(pts + idx);
-  Affine<F> r;
-  uint4* dst = reinterpret_cast<uint4*>(&r);
-#pragma unroll
-  for (int q = 0; q < Q; q++) dst[q] = src[q];
-  return r;
+__global__ void __launch_bounds__(256) k_msm_convert_points(const uint32_t* __restrict__ src, size_t n,
+                                                            Affine<F>* __restrict__ dst) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  dst[i] = load_affine_gnark<F>(src + i * 2 * Coord<F>::WORDS);
 }
 
 template <class F>
@@ -151,7 +137,7 @@ __global__ void __launch_bounds__(128) k_msm_accum(const Affine<F>* __restrict__
       atomicOr(err, 2u);
       continue;
     }
-    Affine<F> P = load_affine(points, idx);
+    Affine<F> P = points[idx];
     if (v >> 31) P.y = fe_neg(P.y);
     xyzz_add_aff(acc, P);
   }
@@ -194,7 +180,7 @@ __global__ void __launch_bounds__(128) k_msm_segmul(XYZZ<F>* __restrict__ segT,
 // Per-window reduction of nseg R_s values: block per window.
 template <class F, int TPB>
 __global__ void __launch_bounds__(TPB) k_msm_winsum(const XYZZ<F>* __restrict__ R, uint32_t nseg,
-                                                    XYZZ<F>* __restrict__ out) {
+                                                    uint32_t* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   XYZZ<F>* sm = reinterpret_cast<XYZZ<F>*>(smem_raw);
   const uint32_t w = blockIdx.x;
@@ -206,7 +192,15 @@ __global__ void __launch_bounds__(TPB) k_msm_winsum(const XYZZ<F>* __restrict__ 
     if ((int)threadIdx.x < half) sm[threadIdx.x] = xyzz_add(sm[threadIdx.x], sm[threadIdx.x + half]);
     __syncthreads();
   }
-  if (threadIdx.x == 0) out[w] = sm[0];
+  if (threadIdx.x == 0) {
+    // window sum in gnark layout (X, Y, ZZ, ZZZ) for the host finish
+    uint32_t* o = out + (size_t)w * 4 * Coord<F>::WORDS;
+    const XYZZ<F> r = sm[0];
+    Coord<F>::store_gnark(o, r.x);
+    Coord<F>::store_gnark(o + Coord<F>::WORDS, r.y);
+    Coord<F>::store_gnark(o + 2 * Coord<F>::WORDS, r.zz);
+    Coord<F>::store_gnark(o + 3 * Coord<F>::WORDS, r.zzz);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -223,7 +217,7 @@ static int choose_window(size_t n) {
 
 template <class C, bool G2>
 int msm_device(gm_ctx* ctx, const void* scalars_dev, const void* points_dev, size_t n,
-               typename GroupSel<C, G2>::HF (&jac_out)[3]) {
+               typename GroupSel<C, G2>::HF (&jac_out)[3], bool points_internal) {
   using DF = typename GroupSel<C, G2>::DF;
   using HF = typename GroupSel<C, G2>::HF;
   using HJ = host::Jac<HF>;
@@ -248,7 +242,8 @@ int msm_device(gm_ctx* ctx, const void* scalars_dev, const void* points_dev, siz
   int rc;
 
   Arena arena(ctx);
-  DevBuf counts, offsets, sorted, buckets, segT, segS, wsum, scan_tmp, errw;
+  constexpr int WORDS = Coord<DF>::WORDS;  // u32 words of one gnark-layout coordinate
+  DevBuf counts, offsets, sorted, buckets, segT, segS, wsum, scan_tmp, errw, ipts;
   if ((rc = errw.alloc(arena, 16))) return rc;
   GM_HIP(hipMemsetAsync(errw.p, 0, 16, st));
   if ((rc = counts.alloc(arena, sizeof(uint32_t) * (total + 1)))) return rc;
@@ -257,7 +252,15 @@ int msm_device(gm_ctx* ctx, const void* scalars_dev, const void* points_dev, siz
   if ((rc = buckets.alloc(arena, sizeof(XYZZ<DF>) * (size_t)total))) return rc;
   if ((rc = segT.alloc(arena, sizeof(XYZZ<DF>) * (size_t)W * nseg))) return rc;
   if ((rc = segS.alloc(arena, sizeof(XYZZ<DF>) * (size_t)W * nseg))) return rc;
-  if ((rc = wsum.alloc(arena, sizeof(XYZZ<DF>) * W))) return rc;
+  if ((rc = wsum.alloc(arena, sizeof(uint32_t) * 4 * WORDS * W))) return rc;
+  const Affine<DF>* pts_internal = reinterpret_cast<const Affine<DF>*>(points_dev);
+  if (!points_internal) {
+    if ((rc = ipts.alloc(arena, sizeof(Affine<DF>) * n))) return rc;
+    ProfScope ps(ctx, "msm_convert_points");
+    hipLaunchKernelGGL(k_msm_convert_points<DF>, dim3(blocks_for(n, 256)), dim3(256), 0, st,
+                       reinterpret_cast<const uint32_t*>(points_dev), n, ipts.as<Affine<DF>>());
+    pts_internal = ipts.as<Affine<DF>>();
+  }
 
   GM_HIP(hipMemsetAsync(counts.p, 0, sizeof(uint32_t) * (total + 1), st));
   const uint32_t* sc = reinterpret_cast<const uint32_t*>(scalars_dev);
@@ -286,10 +289,9 @@ int msm_device(gm_ctx* ctx, const void* scalars_dev, const void* points_dev, siz
   }
   {
     ProfScope ps(ctx, G2 ? "msm_accum_g2" : "msm_accum_g1");
-    hipLaunchKernelGGL(k_msm_accum<DF>, dim3(blocks_for(total, 128)), dim3(128), 0, st,
-                       reinterpret_cast<const Affine<DF>*>(points_dev), (uint32_t)n,
-                       sorted.as<uint32_t>(), offsets.as<uint32_t>(), total, buckets.as<XYZZ<DF>>(),
-                       errw.as<uint32_t>());
+    hipLaunchKernelGGL(k_msm_accum<DF>, dim3(blocks_for(total, 128)), dim3(128), 0, st, pts_internal,
+                       (uint32_t)n, sorted.as<uint32_t>(), offsets.as<uint32_t>(), total,
+                       buckets.as<XYZZ<DF>>(), errw.as<uint32_t>());
   }
   {
     ProfScope ps(ctx, "msm_bucket_reduce");
@@ -299,33 +301,14 @@ int msm_device(gm_ctx* ctx, const void* scalars_dev, const void* points_dev, siz
                        segT.as<XYZZ<DF>>(), segS.as<XYZZ<DF>>(), L, nseg, W);
     constexpr int TPB = 128;
     hipLaunchKernelGGL((k_msm_winsum<DF, TPB>), dim3(W), dim3(TPB), sizeof(XYZZ<DF>) * TPB, st,
-                       segT.as<XYZZ<DF>>(), nseg, wsum.as<XYZZ<DF>>());
+                       segT.as<XYZZ<DF>>(), nseg, wsum.as<uint32_t>());
   }
   GM_HIP(hipGetLastError());
-  if (getenv("GM_DEBUG_MSM")) {
-    GM_HIP(hipStreamSynchronize(st));
-    std::vector<HF> hb(4 * (size_t)total);
-    GM_HIP(hipMemcpy(hb.data(), buckets.p, sizeof(XYZZ<DF>) * total, hipMemcpyDeviceToHost));
-    size_t nonzero = 0;
-    for (size_t b = 0; b < total; b++) nonzero += !hb[4 * b + 2].is_zero();
-    std::vector<uint32_t> off(total + 1);
-    GM_HIP(hipMemcpy(off.data(), offsets.p, 4 * (total + 1), hipMemcpyDeviceToHost));
-    std::vector<HF> ht(4 * (size_t)W * nseg);
-    GM_HIP(hipMemcpy(ht.data(), segT.p, sizeof(XYZZ<DF>) * W * nseg, hipMemcpyDeviceToHost));
-    size_t nzT = 0;
-    for (size_t b = 0; b < (size_t)W * nseg; b++) nzT += !ht[4 * b + 2].is_zero();
-    std::vector<uint32_t> hs(8 * std::min<size_t>(n, 4));
-    GM_HIP(hipMemcpy(hs.data(), scalars_dev, 4 * hs.size(), hipMemcpyDeviceToHost));
-    uint32_t e2 = 0;
-    GM_HIP(hipMemcpy(&e2, errw.p, 4, hipMemcpyDeviceToHost));
-    fprintf(stderr, "[msm dbg] n=%zu c=%u W=%u entries=%u nonzero_buckets=%zu nonzero_R=%zu err=%u s0=%08x%08x\n",
-            n, c, W, off[total], nonzero, nzT, e2, hs[1], hs[0]);
-  }
   uint32_t herr = 0;
   GM_HIP(hipMemcpyAsync(&herr, errw.p, 4, hipMemcpyDeviceToHost, st));
   std::vector<HF> hw(4 * W);
-  static_assert(sizeof(HF) * 4 == sizeof(XYZZ<DF>), "host/device layout mismatch");
-  GM_HIP(hipMemcpyAsync(hw.data(), wsum.p, sizeof(XYZZ<DF>) * W, hipMemcpyDeviceToHost, st));
+  static_assert(sizeof(HF) == 4 * WORDS, "host/device layout mismatch");
+  GM_HIP(hipMemcpyAsync(hw.data(), wsum.p, sizeof(uint32_t) * 4 * WORDS * W, hipMemcpyDeviceToHost, st));
   GM_HIP(hipStreamSynchronize(st));
   if (herr) {
     set_error("msm: internal consistency check failed (code " + std::to_string(herr) + ")");
@@ -345,13 +328,36 @@ int msm_device(gm_ctx* ctx, const void* scalars_dev, const void* points_dev, siz
   return GM_OK;
 }
 
+template <class C, bool G2>
+size_t msm_internal_point_bytes() {
+  return sizeof(Affine<typename GroupSel<C, G2>::DF>);
+}
+
+template <class C, bool G2>
+int msm_prepare_points(gm_ctx* ctx, const void* gnark_points, size_t n, void* dst) {
+  using DF = typename GroupSel<C, G2>::DF;
+  if (n == 0) return GM_OK;
+  hipLaunchKernelGGL(k_msm_convert_points<DF>, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream,
+                     reinterpret_cast<const uint32_t*>(gnark_points), n, reinterpret_cast<Affine<DF>*>(dst));
+  GM_HIP(hipGetLastError());
+  return GM_OK;
+}
+
+#define GM_MSM_PREP_INST(C, G2)                                                   \
+  template size_t msm_internal_point_bytes<C, G2>();                             \
+  template int msm_prepare_points<C, G2>(gm_ctx*, const void*, size_t, void*);
+GM_MSM_PREP_INST(CurveBN254, false)
+GM_MSM_PREP_INST(CurveBN254, true)
+GM_MSM_PREP_INST(CurveBLS12377, false)
+GM_MSM_PREP_INST(CurveBLS12377, true)
+
 template int msm_device<CurveBN254, false>(gm_ctx*, const void*, const void*, size_t,
-                                           CurveBN254::HG1F (&)[3]);
+                                          CurveBN254::HG1F (&)[3], bool);
 template int msm_device<CurveBN254, true>(gm_ctx*, const void*, const void*, size_t,
-                                          CurveBN254::HG2F (&)[3]);
+                                          CurveBN254::HG2F (&)[3], bool);
 template int msm_device<CurveBLS12377, false>(gm_ctx*, const void*, const void*, size_t,
-                                              CurveBLS12377::HG1F (&)[3]);
+                                          CurveBLS12377::HG1F (&)[3], bool);
 template int msm_device<CurveBLS12377, true>(gm_ctx*, const void*, const void*, size_t,
-                                             CurveBLS12377::HG2F (&)[3]);
+                                          CurveBLS12377::HG2F (&)[3], bool);
 
 }  // namespace gm

@@ -24,21 +24,19 @@ constexpr int NTT_TILE = 1 << NTT_TILE_LOG;
 constexpr int NTT_TPB = 256;
 constexpr int NTT_TMAX = 8;
 
+// data vectors: gnark-layout words in HBM, unpacked limbs in registers / LDS
 template <class P>
 GM_DEV Fe<P> ld_fe(const Fe<P>* __restrict__ p, size_t i) {
-  static_assert(sizeof(Fe<P>) == 32, "Fr must be 32 bytes");
-  const uint4* s = reinterpret_cast<const uint4*>(p + i);
-  uint4 a = s[0], b = s[1];
-  Fe<P> r;
-  r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
-  r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
-  return r;
+  return fe_load_g<P>(p, i);
 }
 template <class P>
 GM_DEV void st_fe(Fe<P>* __restrict__ p, size_t i, const Fe<P>& v) {
-  uint4* d = reinterpret_cast<uint4*>(p + i);
-  d[0] = make_uint4(v.v[0], v.v[1], v.v[2], v.v[3]);
-  d[1] = make_uint4(v.v[4], v.v[5], v.v[6], v.v[7]);
+  fe_store_g<P>(p, i, v);
+}
+// device tables (twiddles, coset powers): internal limbs, stored as-is
+template <class P>
+GM_DEV Fe<P> ld_tab(const Fe<P>* __restrict__ t, size_t i) {
+  return t[i];
 }
 
 GM_DEV uint32_t brev_bits(uint32_t x, int bits) { return bits ? (__brev(x) >> (32 - bits)) : 0; }
@@ -57,7 +55,7 @@ __global__ void __launch_bounds__(NTT_TPB) k_ntt_pass(Fe<P>* __restrict__ data, 
   const size_t o0 = (size_t)blockIdx.x * B;
   const size_t lomask = ((size_t)1 << lo) - 1;
 
-  for (int x = threadIdx.x; x < T / 2; x += NTT_TPB) SW[x] = ld_fe(sub, x);
+  for (int x = threadIdx.x; x < T / 2; x += NTT_TPB) SW[x] = ld_tab(sub, x);
 
   // load (j, o) -> X[j*B + o]
   for (int q = threadIdx.x; q < NTT_TILE; q += NTT_TPB) {
@@ -74,7 +72,7 @@ __global__ void __launch_bounds__(NTT_TPB) k_ntt_pass(Fe<P>* __restrict__ data, 
     const size_t hi = o >> lo, L = o & lomask;
     const size_t addr = (hi << (lo + t)) + ((size_t)j << lo) + L;
     Fe<P> v = ld_fe(data, addr);
-    if (DIT && lo > 0) v = fe_mul(v, ld_fe(tw, ((size_t)j << lo) + L));
+    if (DIT && lo > 0) v = fe_mul(v, ld_tab(tw, ((size_t)j << lo) + L));
     X[j * B + ol] = v;
   }
   __syncthreads();
@@ -121,7 +119,7 @@ __global__ void __launch_bounds__(NTT_TPB) k_ntt_pass(Fe<P>* __restrict__ data, 
     const size_t hi = o >> lo, L = o & lomask;
     const size_t addr = (hi << (lo + t)) + ((size_t)j << lo) + L;
     Fe<P> v = X[j * B + ol];
-    if (!DIT && lo > 0) v = fe_mul(v, ld_fe(tw, ((size_t)j << lo) + L));
+    if (!DIT && lo > 0) v = fe_mul(v, ld_tab(tw, ((size_t)j << lo) + L));
     st_fe(data, addr, v);
   }
 }
@@ -141,24 +139,28 @@ GM_DEV Fe<P> fe_pow_u32(const Fe<P>& base, uint32_t e) {
   return r;
 }
 
-// tw[j*2^lo + L] = w^(L * bitrev_t(j)), w = w_{2^(lo+t)} (canonical exponent < 2^(lo+t))
+// tw[j*2^lo + L] = w^(L * bitrev_t(j)), w = w_{2^(lo+t)} (canonical exponent < 2^(lo+t));
+// w arrives in gnark form, tables are written in internal form.
 template <class P>
-__global__ void k_gen_pass_tw(Fe<P>* __restrict__ tw, int lo, int t, Fe<P> w) {
+__global__ void k_gen_pass_tw(Fe<P>* __restrict__ tw, int lo, int t, FeG<P> wg) {
+  const Fe<P> w = fe_to_internal(fe_unpack<P>(wg));
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t size = (size_t)1 << (lo + t);
   if (i >= size) return;
   const uint32_t j = (uint32_t)(i >> lo), L = (uint32_t)(i & (((size_t)1 << lo) - 1));
   const uint64_t e = (uint64_t)L * brev_bits(j, t);
   // e < 2^(lo+t) <= 2^32 for supported sizes
-  st_fe(tw, i, fe_pow_u32(w, (uint32_t)e));
+  tw[i] = fe_pow_u32(w, (uint32_t)e);
 }
 
-// out[x] = base^x * mult, x < count
+// out[x] = base^x * mult, x < count (gnark-form inputs, internal-form table)
 template <class P>
-__global__ void k_gen_powers(Fe<P>* __restrict__ out, size_t count, Fe<P> base, Fe<P> mult) {
+__global__ void k_gen_powers(Fe<P>* __restrict__ out, size_t count, FeG<P> base_g, FeG<P> mult_g) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
-  st_fe(out, i, fe_mul(fe_pow_u32(base, (uint32_t)i), mult));
+  const Fe<P> base = fe_to_internal(fe_unpack<P>(base_g));
+  const Fe<P> mult = fe_to_internal(fe_unpack<P>(mult_g));
+  out[i] = fe_mul(fe_pow_u32(base, (uint32_t)i), mult);
 }
 
 // a[i] *= lo[e & m] * hi[e >> s], e = i or bitrev(i)
@@ -169,23 +171,26 @@ __global__ void __launch_bounds__(256) k_scale_pow(Fe<P>* __restrict__ a, size_t
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t e = BREV ? brev_bits((uint32_t)i, logn) : (uint32_t)i;
-  Fe<P> f = fe_mul(ld_fe(tlo, e & ((1u << s) - 1)), ld_fe(thi, e >> s));
+  Fe<P> f = fe_mul(ld_tab(tlo, e & ((1u << s) - 1)), ld_tab(thi, e >> s));
   st_fe(a, i, fe_mul(ld_fe(a, i), f));
 }
 
 template <class P>
-__global__ void __launch_bounds__(256) k_scale_const(Fe<P>* __restrict__ a, size_t n, Fe<P> k) {
+__global__ void __launch_bounds__(256) k_scale_const(Fe<P>* __restrict__ a, size_t n, FeG<P> kg) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  const Fe<P> k = fe_to_internal(fe_unpack<P>(kg));
   st_fe(a, i, fe_mul(ld_fe(a, i), k));
 }
 
+// a <- (a*b - c) * den, all gnark form: mul(a_g, to_internal(b_g)) = (a*b)_g
 template <class P>
 __global__ void __launch_bounds__(256) k_poly_ops(Fe<P>* __restrict__ a, const Fe<P>* __restrict__ b,
-                                                  const Fe<P>* __restrict__ c, size_t n, Fe<P> den) {
+                                                  const Fe<P>* __restrict__ c, size_t n, FeG<P> den_g) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  Fe<P> v = fe_sub(fe_mul(ld_fe(a, i), ld_fe(b, i)), ld_fe(c, i));
+  const Fe<P> den = fe_to_internal(fe_unpack<P>(den_g));
+  Fe<P> v = fe_sub(fe_mul(ld_fe(a, i), fe_to_internal(ld_fe(b, i))), ld_fe(c, i));
   st_fe(a, i, fe_mul(v, den));
 }
 
@@ -195,9 +200,10 @@ __global__ void __launch_bounds__(256) k_bitrev_swap(Fe<P>* __restrict__ a, size
   if (i >= n) return;
   const size_t r = brev_bits((uint32_t)i, logn);
   if (r > i) {
-    Fe<P> x = ld_fe(a, i), y = ld_fe(a, r);
-    st_fe(a, i, y);
-    st_fe(a, r, x);
+    uint32_t* w = reinterpret_cast<uint32_t*>(a);
+    FeG<P> x = feg_load<P>(w + i * P::NG), y = feg_load<P>(w + r * P::NG);
+    feg_store<P>(w + i * P::NG, y);
+    feg_store<P>(w + r * P::NG, x);
   }
 }
 
@@ -270,8 +276,9 @@ static int domain_build(gm_ctx* ctx, int logn, NttDomain<C>** out) {
   d->ninv = host::finv(host::from_u64<HFr>(d->n));
   d->g = host::from_u64<HFr>(C::COSET_GEN);
   auto dev = [](const HF& h) {
-    Fe<Fr> r;
-    memcpy(r.v, h.v, sizeof(r.v));
+    FeG<Fr> r;
+    static_assert(sizeof(r.w) == sizeof(h.v), "gnark layout");
+    memcpy(r.w, h.v, sizeof(r.w));
     return r;
   };
   int rc;
@@ -295,8 +302,8 @@ static int domain_build(gm_ctx* ctx, int logn, NttDomain<C>** out) {
           wf = wf * wf;
           wi = wi * wi;
         }
-        if ((rc = domain_alloc(d, 32 * sz, &ps.tw_fwd, st))) return rc;
-        if ((rc = domain_alloc(d, 32 * sz, &ps.tw_inv, st))) return rc;
+        if ((rc = domain_alloc(d, sizeof(Fe<Fr>) * sz, &ps.tw_fwd, st))) return rc;
+        if ((rc = domain_alloc(d, sizeof(Fe<Fr>) * sz, &ps.tw_inv, st))) return rc;
         hipLaunchKernelGGL(k_gen_pass_tw<Fr>, dim3(blocks_for(sz, 256)), dim3(256), 0, st,
                            (Fe<Fr>*)ps.tw_fwd, ps.lo, ps.t, dev(wf));
         hipLaunchKernelGGL(k_gen_pass_tw<Fr>, dim3(blocks_for(sz, 256)), dim3(256), 0, st,
@@ -310,8 +317,8 @@ static int domain_build(gm_ctx* ctx, int logn, NttDomain<C>** out) {
           wi = wi * wi;
         }
         size_t cnt = (size_t)1 << (t - 1);
-        if ((rc = domain_alloc(d, 32 * cnt, &d->sub_fwd[t], st))) return rc;
-        if ((rc = domain_alloc(d, 32 * cnt, &d->sub_inv[t], st))) return rc;
+        if ((rc = domain_alloc(d, sizeof(Fe<Fr>) * cnt, &d->sub_fwd[t], st))) return rc;
+        if ((rc = domain_alloc(d, sizeof(Fe<Fr>) * cnt, &d->sub_inv[t], st))) return rc;
         HF one = HF::one();
         hipLaunchKernelGGL(k_gen_powers<Fr>, dim3(blocks_for(cnt, 256)), dim3(256), 0, st,
                            (Fe<Fr>*)d->sub_fwd[t], cnt, dev(wf), dev(one));
@@ -330,10 +337,10 @@ static int domain_build(gm_ctx* ctx, int logn, NttDomain<C>** out) {
     gi_s = gi_s * gi_s;
   }
   HF one = HF::one();
-  if ((rc = domain_alloc(d, 32 * nlo, &d->g_lo, st))) return rc;
-  if ((rc = domain_alloc(d, 32 * nhi, &d->g_hi, st))) return rc;
-  if ((rc = domain_alloc(d, 32 * nlo, &d->gi_lo, st))) return rc;
-  if ((rc = domain_alloc(d, 32 * nhi, &d->gi_hi, st))) return rc;
+  if ((rc = domain_alloc(d, sizeof(Fe<Fr>) * nlo, &d->g_lo, st))) return rc;
+  if ((rc = domain_alloc(d, sizeof(Fe<Fr>) * nhi, &d->g_hi, st))) return rc;
+  if ((rc = domain_alloc(d, sizeof(Fe<Fr>) * nlo, &d->gi_lo, st))) return rc;
+  if ((rc = domain_alloc(d, sizeof(Fe<Fr>) * nhi, &d->gi_hi, st))) return rc;
   hipLaunchKernelGGL(k_gen_powers<Fr>, dim3(blocks_for(nlo, 256)), dim3(256), 0, st, (Fe<Fr>*)d->g_lo,
                      nlo, dev(d->g), dev(one));
   hipLaunchKernelGGL(k_gen_powers<Fr>, dim3(blocks_for(nhi, 256)), dim3(256), 0, st, (Fe<Fr>*)d->g_hi,
@@ -431,8 +438,8 @@ int ntt_device(gm_ctx* ctx, void* data, size_t n, bool inverse, bool dit, bool c
         hipLaunchKernelGGL((k_scale_pow<Fr, true>), dim3(g), dim3(256), 0, st, a, n, logn,
                            (const Fe<Fr>*)d->gi_lo, (const Fe<Fr>*)d->gi_hi, d->cs);
     } else {
-      Fe<Fr> k;
-      memcpy(k.v, d->ninv.v, sizeof(k.v));
+      FeG<Fr> k;
+      memcpy(k.w, d->ninv.v, sizeof(k.w));
       hipLaunchKernelGGL(k_scale_const<Fr>, dim3(g), dim3(256), 0, st, a, n, k);
     }
   }
@@ -443,8 +450,8 @@ int ntt_device(gm_ctx* ctx, void* data, size_t n, bool inverse, bool dit, bool c
 template <class C>
 int poly_ops_device(gm_ctx* ctx, void* a, const void* b, const void* c, size_t n, const void* den_host) {
   using Fr = typename C::Fr;
-  Fe<Fr> den;
-  memcpy(den.v, den_host, sizeof(den.v));
+  FeG<Fr> den;
+  memcpy(den.w, den_host, sizeof(den.w));
   ProfScope ps(ctx, "poly_ops");
   hipLaunchKernelGGL(k_poly_ops<Fr>, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream,
                      (Fe<Fr>*)a, (const Fe<Fr>*)b, (const Fe<Fr>*)c, n, den);

@@ -6,14 +6,15 @@
 
 namespace gm {
 
+// gnark-layout element i -> internal, and back
 template <class F>
 struct ElemIO {
   GM_DEV static F load(const uint8_t* p, size_t i) {
-    F r;
-    memcpy(&r, p + sizeof(F) * i, sizeof(F));
-    return r;
+    return Coord<F>::load_internal(reinterpret_cast<const uint32_t*>(p) + i * Coord<F>::WORDS);
   }
-  GM_DEV static void store(uint8_t* p, size_t i, const F& v) { memcpy(p + sizeof(F) * i, &v, sizeof(F)); }
+  GM_DEV static void store(uint8_t* p, size_t i, const F& v) {
+    Coord<F>::store_gnark(reinterpret_cast<uint32_t*>(p) + i * Coord<F>::WORDS, v);
+  }
 };
 
 template <class F>
@@ -55,10 +56,11 @@ GM_DEV XYZZ<F> from_affine_dev(const Affine<F>& p) {
 }
 
 template <class F>
-__global__ void k_point_op(int op, const Affine<F>* a, const Affine<F>* b, Affine<F>* out, size_t n) {
+__global__ void k_point_op(int op, const uint32_t* a, const uint32_t* b, uint32_t* out, size_t n) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  Affine<F> p = a[i], q = b[i];
+  constexpr int PW = 2 * Coord<F>::WORDS;
+  Affine<F> p = load_affine_gnark<F>(a + i * PW), q = load_affine_gnark<F>(b + i * PW);
   XYZZ<F> r;
   switch (op) {
     case 0: r = from_affine_dev(p); xyzz_add_aff(r, q); break;          // mixed add
@@ -67,7 +69,7 @@ __global__ void k_point_op(int op, const Affine<F>* a, const Affine<F>* b, Affin
     case 3: r = xyzz_mul_small(from_affine_dev(p), 1000003u); break;      // small scalar mul
     default: r = from_affine_dev(p); break;
   }
-  out[i] = to_affine_dev(r);
+  store_affine_gnark<F>(out + i * PW, to_affine_dev(r));
 }
 
 }  // namespace gm
@@ -91,7 +93,7 @@ template <class C, bool G2>
 static int point_op_t(gm_ctx* ctx, int op, const void* a, const void* b, void* out, size_t n) {
   using DF = typename GroupSel<C, G2>::DF;
   hipLaunchKernelGGL(k_point_op<DF>, dim3(blocks_for(n, 64)), dim3(64), 0, ctx->stream, op,
-                     (const Affine<DF>*)a, (const Affine<DF>*)b, (Affine<DF>*)out, n);
+                     (const uint32_t*)a, (const uint32_t*)b, (uint32_t*)out, n);
   GM_HIP(hipGetLastError());
   GM_HIP(hipStreamSynchronize(ctx->stream));
   return GM_OK;
