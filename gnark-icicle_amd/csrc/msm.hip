@@ -107,6 +107,52 @@ __global__ void __launch_bounds__(256) k_msm_scatter(const uint32_t* __restrict_
   }
 }
 
+// Digit keys for a radix sort: key = global bucket index w*nb + |d|-1 (or the
+// sentinel `total` for a zero digit, which sorts past every bucket), value =
+// point index | sign << 31.  Window-major: entry (w, i) at w*n + i.
+template <class Fr>
+__global__ void __launch_bounds__(256) k_msm_keys(const uint32_t* __restrict__ scalars, uint32_t n,
+                                                  uint32_t c, uint32_t W, uint32_t* __restrict__ keys,
+                                                  uint32_t* __restrict__ vals) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const FeG<Fr> k = load_scalar_canonical<Fr>(scalars, i);
+  const uint32_t nb = 1u << (c - 1), mask = (1u << c) - 1, total = W * nb;
+  uint32_t carry = 0;
+  for (uint32_t w = 0; w < W; w++) {
+    const uint32_t raw = window_bits(k, w * c, mask) + carry;
+    uint32_t d, neg;
+    if (raw > nb) {
+      d = (1u << c) - raw;
+      carry = 1;
+      neg = 1;
+    } else {
+      d = raw;
+      carry = 0;
+      neg = 0;
+    }
+    const size_t e = (size_t)w * n + i;
+    keys[e] = d ? w * nb + d - 1 : total;
+    vals[e] = i | (neg << 31);
+  }
+}
+
+// offsets[b] = first sorted position with key >= b, for b in [0, total].
+__global__ void __launch_bounds__(256) k_msm_offsets(const uint32_t* __restrict__ keys, size_t M,
+                                                     uint32_t total, uint32_t* __restrict__ offsets) {
+  const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= M) return;
+  const uint32_t k = keys[q];
+  const uint32_t kp = q ? keys[q - 1] : 0xffffffffu;  // -1
+  if (k != kp) {
+    const uint32_t lo = kp == 0xffffffffu ? 0 : kp + 1;
+    const uint32_t hi = k < total ? k : total;
+    for (uint32_t b = lo; b <= hi; b++) offsets[b] = (uint32_t)q;
+  }
+  if (q == M - 1 && k < total)
+    for (uint32_t b = k + 1; b <= total; b++) offsets[b] = (uint32_t)M;
+}
+
 // ---------------------------------------------------------------------------
 // points: gnark layout -> internal layout (once per MSM, into workspace)
 // ---------------------------------------------------------------------------
@@ -141,6 +187,96 @@ __global__ void __launch_bounds__(128) k_msm_accum(const Affine<F>* __restrict__
     if (v >> 31) P.y = fe_neg(P.y);
     xyzz_add_aff(acc, P);
   }
+  buckets[b] = acc;
+}
+
+// Load-balanced accumulation over the sorted entry list: thread t owns entries
+// [t*K, t*K+K).  A bucket whose whole range lies in the thread's slice is
+// written straight to `buckets`; the (at most two) buckets cut by the slice
+// edges go to part_first[t] / part_last[t] and are merged by k_msm_fixup.
+// Skewed scalar distributions (one huge bucket) therefore cost the same as
+// uniform ones in this phase.
+template <class F>
+GM_DEV void accum_emit(uint32_t b, const XYZZ<F>& acc, bool is_first, bool is_last, uint32_t start,
+                       uint32_t end, uint32_t t, const uint32_t* __restrict__ offsets,
+                       XYZZ<F>* __restrict__ buckets, XYZZ<F>* __restrict__ part_first,
+                       XYZZ<F>* __restrict__ part_last) {
+  const uint32_t bs = offsets[b], be = offsets[b + 1];
+  if (bs >= start && be <= end) {
+    buckets[b] = acc;
+  } else {
+    if (is_first) part_first[t] = acc;
+    if (is_last) part_last[t] = acc;
+  }
+}
+
+template <class F>
+__global__ void __launch_bounds__(128) k_msm_accum_seg(const Affine<F>* __restrict__ points, uint32_t n,
+                                                       const uint32_t* __restrict__ keys,
+                                                       const uint32_t* __restrict__ vals,
+                                                       const uint32_t* __restrict__ offsets, uint32_t total,
+                                                       uint32_t K, XYZZ<F>* __restrict__ buckets,
+                                                       XYZZ<F>* __restrict__ part_first,
+                                                       XYZZ<F>* __restrict__ part_last,
+                                                       uint32_t* __restrict__ err) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t Mv = offsets[total];  // valid (non-zero-digit) entries
+  const uint32_t start = t * K;
+  if (start >= Mv) return;
+  const uint32_t end = min(start + K, Mv);
+  uint32_t cur = keys[start];
+  bool first = true;
+  XYZZ<F> acc = xyzz_inf<F>();
+  uint32_t v = vals[start];
+  uint32_t idx = v & 0x7fffffffu;
+  if (idx >= n) {
+    atomicOr(err, 2u);
+    return;
+  }
+  Affine<F> P = points[idx];
+  for (uint32_t q = start; q < end; q++) {
+    const uint32_t k = keys[q];
+    // prefetch the next point while this add runs
+    uint32_t vn = 0;
+    Affine<F> Pn;
+    if (q + 1 < end) {
+      vn = vals[q + 1];
+      const uint32_t in = vn & 0x7fffffffu;
+      if (in >= n) {
+        atomicOr(err, 2u);
+        return;
+      }
+      Pn = points[in];
+    }
+    if (k != cur) {
+      accum_emit(cur, acc, first, false, start, end, t, offsets, buckets, part_first, part_last);
+      first = false;
+      acc = xyzz_inf<F>();
+      cur = k;
+    }
+    if (v >> 31) P.y = fe_neg(P.y);
+    xyzz_add_aff(acc, P);
+    v = vn;
+    P = Pn;
+  }
+  accum_emit(cur, acc, first, true, start, end, t, offsets, buckets, part_first, part_last);
+}
+
+// Merge the partial sums of buckets cut by slice edges (bucket b spans slices t0..t1).
+template <class F>
+__global__ void __launch_bounds__(128) k_msm_fixup(const uint32_t* __restrict__ offsets, uint32_t total,
+                                                   uint32_t K, XYZZ<F>* __restrict__ buckets,
+                                                   const XYZZ<F>* __restrict__ part_first,
+                                                   const XYZZ<F>* __restrict__ part_last) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= total) return;
+  const uint32_t bs = offsets[b], be = offsets[b + 1];
+  if (be == bs) return;
+  const uint32_t t0 = bs / K, t1 = (be - 1) / K;
+  if (t0 == t1) return;
+  XYZZ<F> acc = part_last[t0];
+  for (uint32_t t = t0 + 1; t < t1; t++) acc = xyzz_add(acc, part_first[t]);
+  acc = xyzz_add(acc, part_first[t1]);
   buckets[b] = acc;
 }
 
@@ -243,10 +379,13 @@ int msm_device(gm_ctx* ctx, const void* scalars_dev, const void* points_dev, siz
 
   Arena arena(ctx);
   constexpr int WORDS = Coord<DF>::WORDS;  // u32 words of one gnark-layout coordinate
-  DevBuf counts, offsets, sorted, buckets, segT, segS, wsum, scan_tmp, errw, ipts;
+  DevBuf counts, offsets, sorted, buckets, segT, segS, wsum, scan_tmp, errw, ipts, keys_in, keys_out;
   if ((rc = errw.alloc(arena, 16))) return rc;
   GM_HIP(hipMemsetAsync(errw.p, 0, 16, st));
-  if ((rc = counts.alloc(arena, sizeof(uint32_t) * (total + 1)))) return rc;
+  // counts doubles as the unsorted value array of the radix sort
+  if ((rc = counts.alloc(arena, sizeof(uint32_t) * (size_t)W * n))) return rc;
+  if ((rc = keys_in.alloc(arena, sizeof(uint32_t) * (size_t)W * n))) return rc;
+  if ((rc = keys_out.alloc(arena, sizeof(uint32_t) * (size_t)W * n))) return rc;
   if ((rc = offsets.alloc(arena, sizeof(uint32_t) * (total + 1)))) return rc;
   if ((rc = sorted.alloc(arena, sizeof(uint32_t) * (size_t)W * n))) return rc;
   if ((rc = buckets.alloc(arena, sizeof(XYZZ<DF>) * (size_t)total))) return rc;
@@ -262,36 +401,50 @@ int msm_device(gm_ctx* ctx, const void* scalars_dev, const void* points_dev, siz
     pts_internal = ipts.as<Affine<DF>>();
   }
 
-  GM_HIP(hipMemsetAsync(counts.p, 0, sizeof(uint32_t) * (total + 1), st));
   const uint32_t* sc = reinterpret_cast<const uint32_t*>(scalars_dev);
+  const size_t M = (size_t)W * n;
+  if (M >= (size_t(1) << 31)) {
+    set_error("msm: n * windows must be < 2^31");
+    return GM_ERR_INVALID;
+  }
   {
-    ProfScope ps(ctx, "msm_hist");
-    hipLaunchKernelGGL(k_msm_hist<typename C::Fr>, dim3(blocks_for(n, 256)), dim3(256), 0, st, sc,
-                       (uint32_t)n, c, W, counts.as<uint32_t>());
+    ProfScope ps(ctx, "msm_keys");
+    hipLaunchKernelGGL(k_msm_keys<typename C::Fr>, dim3(blocks_for(n, 256)), dim3(256), 0, st, sc,
+                       (uint32_t)n, c, W, keys_in.as<uint32_t>(), counts.as<uint32_t>());
   }
   GM_HIP(hipGetLastError());
+  int end_bit = 1;
+  while ((1ull << end_bit) <= total) end_bit++;
   size_t tmp_bytes = 0;
-  GM_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, counts.as<uint32_t>(),
-                                          offsets.as<uint32_t>(), total + 1, st));
+  GM_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys_in.as<uint32_t>(), keys_out.as<uint32_t>(),
+                                            counts.as<uint32_t>(), sorted.as<uint32_t>(), (int)M, 0, end_bit, st));
   if ((rc = scan_tmp.alloc(arena, tmp_bytes))) return rc;
   {
-    ProfScope ps(ctx, "msm_scan");
-    GM_HIP(hipcub::DeviceScan::ExclusiveSum(scan_tmp.p, tmp_bytes, counts.as<uint32_t>(),
-                                            offsets.as<uint32_t>(), total + 1, st));
-  }
-  // cursor = offsets (reuse counts buffer)
-  GM_HIP(hipMemcpyAsync(counts.p, offsets.p, sizeof(uint32_t) * (total + 1), hipMemcpyDeviceToDevice, st));
-  {
-    ProfScope ps(ctx, "msm_scatter");
-    hipLaunchKernelGGL(k_msm_scatter<typename C::Fr>, dim3(blocks_for(n, 256)), dim3(256), 0, st, sc,
-                       (uint32_t)n, c, W, counts.as<uint32_t>(), offsets.as<uint32_t>() + 1,
-                       sorted.as<uint32_t>(), errw.as<uint32_t>());
+    ProfScope ps(ctx, "msm_sort");
+    GM_HIP(hipcub::DeviceRadixSort::SortPairs(scan_tmp.p, tmp_bytes, keys_in.as<uint32_t>(),
+                                              keys_out.as<uint32_t>(), counts.as<uint32_t>(),
+                                              sorted.as<uint32_t>(), (int)M, 0, end_bit, st));
   }
   {
+    ProfScope ps(ctx, "msm_offsets");
+    hipLaunchKernelGGL(k_msm_offsets, dim3(blocks_for(M, 256)), dim3(256), 0, st, keys_out.as<uint32_t>(), M,
+                       total, offsets.as<uint32_t>());
+  }
+  GM_HIP(hipGetLastError());
+  {
+    const uint32_t K = ctx->msm_slice ? (uint32_t)ctx->msm_slice : 64u;
+    const size_t nslices = (M + K - 1) / K;
+    DevBuf pfirst, plast;
+    if ((rc = pfirst.alloc(arena, sizeof(XYZZ<DF>) * nslices))) return rc;
+    if ((rc = plast.alloc(arena, sizeof(XYZZ<DF>) * nslices))) return rc;
+    GM_HIP(hipMemsetAsync(buckets.p, 0, sizeof(XYZZ<DF>) * (size_t)total, st));  // all-zero XYZZ = infinity
     ProfScope ps(ctx, G2 ? "msm_accum_g2" : "msm_accum_g1");
-    hipLaunchKernelGGL(k_msm_accum<DF>, dim3(blocks_for(total, 128)), dim3(128), 0, st, pts_internal,
-                       (uint32_t)n, sorted.as<uint32_t>(), offsets.as<uint32_t>(), total,
-                       buckets.as<XYZZ<DF>>(), errw.as<uint32_t>());
+    hipLaunchKernelGGL(k_msm_accum_seg<DF>, dim3(blocks_for(nslices, 128)), dim3(128), 0, st, pts_internal,
+                       (uint32_t)n, keys_out.as<uint32_t>(), sorted.as<uint32_t>(), offsets.as<uint32_t>(), total,
+                       K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>(),
+                       errw.as<uint32_t>());
+    hipLaunchKernelGGL(k_msm_fixup<DF>, dim3(blocks_for(total, 128)), dim3(128), 0, st, offsets.as<uint32_t>(),
+                       total, K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>());
   }
   {
     ProfScope ps(ctx, "msm_bucket_reduce");

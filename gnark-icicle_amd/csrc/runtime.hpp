@@ -48,6 +48,7 @@ struct gm_ctx {
   // cached NTT domains: key = curve*64 + logn
   std::map<int, void*> ntt_domains;
   int msm_c_override = 0;
+  int msm_slice = 0;  // entries per thread in the bucket accumulation (0 = default)
   // workspace arena: chunks of hipMalloc'd memory, stack-discipline scopes
   struct Chunk {
     char* base;
