@@ -1,11 +1,16 @@
 // MSM entry points (see msm.hip).
 #pragma once
 #include <cstddef>
+#include <cstdint>
 #include "curves.hpp"
 
 struct gm_ctx;
 
 namespace gm {
+struct Arena;
+// Sorts M (key, value) u32 pairs by the low end_bit key bits (msm_sort.hip).
+int msm_sort_pairs(gm_ctx* ctx, Arena& arena, const uint32_t* keys_in, uint32_t* keys_out,
+                   const uint32_t* vals_in, uint32_t* vals_out, size_t M, int end_bit);
 // out = sum_i int(scalars[i]) * points[i] as a host Jacobian triple (X, Y, Z).
 // points_dev is gnark-layout affine points, or (points_internal) an array of
 // device-internal Affine<F> (radix-2^29 Montgomery) prepared by

@@ -1,0 +1,6 @@
+// Pippenger MSM instantiation: CurveBLS12377 G1 (templates in msm_impl.hpp).
+#include "msm_impl.hpp"
+
+namespace gm {
+GM_MSM_INSTANTIATE(CurveBLS12377, false)
+}  // namespace gm

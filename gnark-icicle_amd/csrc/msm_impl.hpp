@@ -1,3 +1,4 @@
+#pragma once
 // Pippenger bucket MSM on gfx950 -- replaces iciclegnark MsmOnDevice /
 // MsmG2OnDevice (backend/groth16/bn254/icicle/icicle.go:302,315,332,355,382).
 //
@@ -17,8 +18,6 @@
 //
 // Exact group arithmetic: the result is independent of summation order, so the
 // atomics-based counting sort needs no determinism.
-#include <hipcub/hipcub.hpp>
-
 #include "curves.hpp"
 #include "msm.hpp"
 #include "runtime.hpp"
@@ -45,66 +44,6 @@ GM_DEV uint32_t window_bits(const FeG<Fr>& k, uint32_t bit, uint32_t mask) {
 template <class Fr>
 GM_DEV FeG<Fr> load_scalar_canonical(const uint32_t* __restrict__ s, uint32_t i) {
   return fe_pack(fe_gnark_to_canonical(fe_load_g<Fr>(s, i)));
-}
-
-// Signed digit recoding: raw = bits + carry; raw > 2^(c-1) -> digit raw - 2^c.
-// Digits lie in [-(2^(c-1) - 1), 2^(c-1)]; bucket index = |digit| - 1.
-template <class Fr>
-__global__ void __launch_bounds__(256) k_msm_hist(const uint32_t* __restrict__ scalars, uint32_t n,
-                                                  uint32_t c, uint32_t W,
-                                                  uint32_t* __restrict__ counts) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const FeG<Fr> k = load_scalar_canonical<Fr>(scalars, i);
-  const uint32_t nb = 1u << (c - 1), mask = (1u << c) - 1;
-  uint32_t carry = 0;
-  for (uint32_t w = 0; w < W; w++) {
-    uint32_t raw = window_bits(k, w * c, mask) + carry;
-    uint32_t d;
-    if (raw > nb) {
-      d = (1u << c) - raw;
-      carry = 1;
-    } else {
-      d = raw;
-      carry = 0;
-    }
-    if (d) atomicAdd(&counts[w * nb + d - 1], 1u);
-  }
-}
-
-template <class Fr>
-__global__ void __launch_bounds__(256) k_msm_scatter(const uint32_t* __restrict__ scalars,
-                                                     uint32_t n, uint32_t c, uint32_t W,
-                                                     uint32_t* __restrict__ cursor,
-                                                     const uint32_t* __restrict__ bucket_end,
-                                                     uint32_t* __restrict__ sorted,
-                                                     uint32_t* __restrict__ err) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const FeG<Fr> k = load_scalar_canonical<Fr>(scalars, i);
-  const uint32_t nb = 1u << (c - 1), mask = (1u << c) - 1;
-  uint32_t carry = 0;
-  for (uint32_t w = 0; w < W; w++) {
-    uint32_t raw = window_bits(k, w * c, mask) + carry;
-    uint32_t d, neg;
-    if (raw > nb) {
-      d = (1u << c) - raw;
-      carry = 1;
-      neg = 1;
-    } else {
-      d = raw;
-      carry = 0;
-      neg = 0;
-    }
-    if (d) {
-      const uint32_t b = w * nb + d - 1;
-      const uint32_t pos = atomicAdd(&cursor[b], 1u);
-      if (pos < bucket_end[b])
-        sorted[pos] = i | (neg << 31);
-      else
-        atomicOr(err, 1u);  // histogram / scatter disagreement: never write out of range
-    }
-  }
 }
 
 // Digit keys for a radix sort: key = global bucket index w*nb + |d|-1 (or the
@@ -137,22 +76,6 @@ __global__ void __launch_bounds__(256) k_msm_keys(const uint32_t* __restrict__ s
   }
 }
 
-// offsets[b] = first sorted position with key >= b, for b in [0, total].
-__global__ void __launch_bounds__(256) k_msm_offsets(const uint32_t* __restrict__ keys, size_t M,
-                                                     uint32_t total, uint32_t* __restrict__ offsets) {
-  const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= M) return;
-  const uint32_t k = keys[q];
-  const uint32_t kp = q ? keys[q - 1] : 0xffffffffu;  // -1
-  if (k != kp) {
-    const uint32_t lo = kp == 0xffffffffu ? 0 : kp + 1;
-    const uint32_t hi = k < total ? k : total;
-    for (uint32_t b = lo; b <= hi; b++) offsets[b] = (uint32_t)q;
-  }
-  if (q == M - 1 && k < total)
-    for (uint32_t b = k + 1; b <= total; b++) offsets[b] = (uint32_t)M;
-}
-
 // ---------------------------------------------------------------------------
 // points: gnark layout -> internal layout (once per MSM, into workspace)
 // ---------------------------------------------------------------------------
@@ -162,32 +85,6 @@ __global__ void __launch_bounds__(256) k_msm_convert_points(const uint32_t* __re
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   dst[i] = load_affine_gnark<F>(src + i * 2 * Coord<F>::WORDS);
-}
-
-template <class F>
-__global__ void __launch_bounds__(128) k_msm_accum(const Affine<F>* __restrict__ points,
-                                                   uint32_t n,
-                                                   const uint32_t* __restrict__ sorted,
-                                                   const uint32_t* __restrict__ offsets,
-                                                   uint32_t total_buckets,
-                                                   XYZZ<F>* __restrict__ buckets,
-                                                   uint32_t* __restrict__ err) {
-  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= total_buckets) return;
-  const uint32_t s = offsets[b], e = offsets[b + 1];
-  XYZZ<F> acc = xyzz_inf<F>();
-  for (uint32_t q = s; q < e; q++) {
-    const uint32_t v = sorted[q];
-    const uint32_t idx = v & 0x7fffffffu;
-    if (idx >= n) {
-      atomicOr(err, 2u);
-      continue;
-    }
-    Affine<F> P = points[idx];
-    if (v >> 31) P.y = fe_neg(P.y);
-    xyzz_add_aff(acc, P);
-  }
-  buckets[b] = acc;
 }
 
 // Load-balanced accumulation over the sorted entry list: thread t owns entries
@@ -280,63 +177,113 @@ __global__ void __launch_bounds__(128) k_msm_fixup(const uint32_t* __restrict__ 
   buckets[b] = acc;
 }
 
-// Segment running sums.  Segment s of window w covers bucket array indices
-// j in [s*L, s*L + L) (bucket weight j+1):
-//   S_s = sum_j B_j,   T_s = sum_j (j - s*L + 1) B_j
+// ---------------------------------------------------------------------------
+// Bucket reduction: window sum P_w = sum_j (j+1) B_j over the nb buckets of a
+// window.  A single EC add costs ~15-20 us of latency in one wave, so the
+// reduction is organised to keep every serial chain short and all 1024 SIMDs
+// busy, and to leave the inherently serial Horner tail (~W*c doublings) to the
+// host, where one group op is ~50x cheaper in latency:
+//
+//   level 1 (k_msm_seg): segments of L buckets, running sums
+//        S_s = sum_l B_{sL+l},  T_s = sum_l (l+1) B_{sL+l}
+//     so P_w = sum_s T_s + L * sum_s s*S_s.
+//   levels 2.. (k_msm_bitsum): LDS trees over the segments that never multiply
+//     by the index: a node carries [G, U, Y_0..Y_{K-1}] with G = sum S, U = sum T
+//     and Y_b = sum of S over the node's segments whose local index has bit b
+//     set.  Merging two sibling nodes of 2^d segments is (K+3) independent adds
+//     (Y_d of the parent is G of the right child), one per thread, so a tree
+//     over NT segments has depth log2(NT) adds and ~3 adds of work per segment.
+//   host: P_w = U + sum_b 2^(b + log2 L) Y_b, merged into the window Horner.
+// ---------------------------------------------------------------------------
+// node layout: per window, m nodes of Q = 2 + K XYZZ points [G, U, Y_0..Y_{K-1}]
 template <class F>
-__global__ void __launch_bounds__(128) k_msm_seg(const XYZZ<F>* __restrict__ buckets,
-                                                 uint32_t nb, uint32_t L, uint32_t nseg,
-                                                 uint32_t W, XYZZ<F>* __restrict__ segT,
-                                                 XYZZ<F>* __restrict__ segS) {
+__global__ void __launch_bounds__(128) k_msm_seg(const XYZZ<F>* __restrict__ buckets, uint32_t nb,
+                                                 uint32_t L, uint32_t nseg, uint32_t W,
+                                                 XYZZ<F>* __restrict__ nodes) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= W * nseg) return;
   const uint32_t w = t / nseg, s = t % nseg;
   const XYZZ<F>* B = buckets + (size_t)w * nb + (size_t)s * L;
-  XYZZ<F> S = xyzz_inf<F>(), T = xyzz_inf<F>();
-  for (int j = (int)L - 1; j >= 0; j--) {
+  XYZZ<F> S = B[L - 1], T = S;
+  for (int j = (int)L - 2; j >= 0; j--) {
     S = xyzz_add(S, B[j]);
     T = xyzz_add(T, S);
   }
-  segT[t] = T;
-  segS[t] = S;
+  nodes[2 * (size_t)t] = S;
+  nodes[2 * (size_t)t + 1] = T;
 }
 
-// R_s = T_s + (s*L) * S_s
+// One tree level group: block (w, j) merges nodes [j*NT, (j+1)*NT) of window w
+// (Qin points each) into one node of Qin + log2(NT) points.
 template <class F>
-__global__ void __launch_bounds__(128) k_msm_segmul(XYZZ<F>* __restrict__ segT,
-                                                    const XYZZ<F>* __restrict__ segS, uint32_t L,
-                                                    uint32_t nseg, uint32_t W) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= W * nseg) return;
-  const uint32_t s = t % nseg;
-  XYZZ<F> m = xyzz_mul_small(segS[t], s * L);
-  segT[t] = xyzz_add(segT[t], m);
-}
-
-// Per-window reduction of nseg R_s values: block per window.
-template <class F, int TPB>
-__global__ void __launch_bounds__(TPB) k_msm_winsum(const XYZZ<F>* __restrict__ R, uint32_t nseg,
-                                                    uint32_t* __restrict__ out) {
+__global__ void __launch_bounds__(256) k_msm_bitsum(const XYZZ<F>* __restrict__ in, uint32_t m,
+                                                    uint32_t Qin, uint32_t NT, uint32_t lgNT,
+                                                    XYZZ<F>* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  XYZZ<F>* sm = reinterpret_cast<XYZZ<F>*>(smem_raw);
-  const uint32_t w = blockIdx.x;
-  XYZZ<F> acc = xyzz_inf<F>();
-  for (uint32_t s = threadIdx.x; s < nseg; s += TPB) acc = xyzz_add(acc, R[(size_t)w * nseg + s]);
-  sm[threadIdx.x] = acc;
+  XYZZ<F>* X = reinterpret_cast<XYZZ<F>*>(smem_raw);
+  const uint32_t groups = m / NT;
+  const uint32_t w = blockIdx.x / groups, j = blockIdx.x % groups;
+  const XYZZ<F>* src = in + ((size_t)w * m + (size_t)j * NT) * Qin;
+  for (uint32_t q = threadIdx.x; q < NT * Qin; q += blockDim.x) X[q] = src[q];
   __syncthreads();
-  for (int half = TPB / 2; half > 0; half >>= 1) {
-    if ((int)threadIdx.x < half) sm[threadIdx.x] = xyzz_add(sm[threadIdx.x], sm[threadIdx.x + half]);
+  for (uint32_t d = 0; d < lgNT; d++) {
+    const uint32_t qc = Qin + d + 1;           // quantities of a parent node
+    const uint32_t tasks = (NT >> (d + 1)) * qc;
+    const uint32_t child = (Qin << d);          // slots spanned by one child
+    XYZZ<F> r0, r1;
+    uint32_t s0 = 0xffffffffu, s1 = 0xffffffffu;
+    {
+      const uint32_t t = threadIdx.x;
+      if (t < tasks) {
+        const uint32_t p = t / qc, q = t % qc, base = p * 2 * child;
+        r0 = (q + 1 < qc) ? xyzz_add(X[base + q], X[base + child + q]) : X[base + child];
+        s0 = base + q;
+      }
+    }
+    {
+      const uint32_t t = threadIdx.x + blockDim.x;
+      if (t < tasks) {
+        const uint32_t p = t / qc, q = t % qc, base = p * 2 * child;
+        r1 = (q + 1 < qc) ? xyzz_add(X[base + q], X[base + child + q]) : X[base + child];
+        s1 = base + q;
+      }
+    }
+    __syncthreads();
+    if (s0 != 0xffffffffu) X[s0] = r0;
+    if (s1 != 0xffffffffu) X[s1] = r1;
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    // window sum in gnark layout (X, Y, ZZ, ZZZ) for the host finish
-    uint32_t* o = out + (size_t)w * 4 * Coord<F>::WORDS;
-    const XYZZ<F> r = sm[0];
-    Coord<F>::store_gnark(o, r.x);
-    Coord<F>::store_gnark(o + Coord<F>::WORDS, r.y);
-    Coord<F>::store_gnark(o + 2 * Coord<F>::WORDS, r.zz);
-    Coord<F>::store_gnark(o + 3 * Coord<F>::WORDS, r.zzz);
+  const uint32_t Qout = Qin + lgNT;
+  XYZZ<F>* dst = out + ((size_t)w * groups + j) * Qout;
+  for (uint32_t q = threadIdx.x; q < Qout; q += blockDim.x) dst[q] = X[q];
+}
+
+// internal XYZZ -> gnark-layout (X, Y, ZZ, ZZZ) words for the host finish
+template <class F>
+__global__ void __launch_bounds__(128) k_msm_export(const XYZZ<F>* __restrict__ nodes, uint32_t count,
+                                                    uint32_t* __restrict__ out) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= count) return;
+  uint32_t* o = out + (size_t)t * 4 * Coord<F>::WORDS;
+  const XYZZ<F> r = nodes[t];
+  Coord<F>::store_gnark(o, r.x);
+  Coord<F>::store_gnark(o + Coord<F>::WORDS, r.y);
+  Coord<F>::store_gnark(o + 2 * Coord<F>::WORDS, r.zz);
+  Coord<F>::store_gnark(o + 3 * Coord<F>::WORDS, r.zzz);
+}
+
+// offsets[b] = first sorted position with key >= b (lower bound), b in [0, total]
+static __global__ void __launch_bounds__(256) k_msm_lower_bound(const uint32_t* __restrict__ keys, uint32_t M,
+                                                         uint32_t total, uint32_t* __restrict__ offsets) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b > total) return;
+  uint32_t lo = 0, hi = M;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (keys[mid] < b) lo = mid + 1;
+    else hi = mid;
   }
+  offsets[b] = lo;
 }
 
 // ---------------------------------------------------------------------------
@@ -373,13 +320,13 @@ int msm_device(gm_ctx* ctx, const void* scalars_dev, const void* points_dev, siz
   const uint32_t W = (C::FR_BITS + 1 + c - 1) / c;  // ceil((bits+1)/c): top signed digit never carries
   const uint32_t nb = 1u << (c - 1);
   const uint32_t total = W * nb;
-  const uint32_t L = nb >= 64 ? 8 : 1;
+  const uint32_t L = nb >= 4 ? 4 : nb;  // level-1 segment length (buckets)
   const uint32_t nseg = nb / L;
   int rc;
 
   Arena arena(ctx);
   constexpr int WORDS = Coord<DF>::WORDS;  // u32 words of one gnark-layout coordinate
-  DevBuf counts, offsets, sorted, buckets, segT, segS, wsum, scan_tmp, errw, ipts, keys_in, keys_out;
+  DevBuf counts, offsets, sorted, buckets, nodes_a, nodes_b, wsum, errw, ipts, keys_in, keys_out;
   if ((rc = errw.alloc(arena, 16))) return rc;
   GM_HIP(hipMemsetAsync(errw.p, 0, 16, st));
   // counts doubles as the unsorted value array of the radix sort
@@ -389,9 +336,9 @@ int msm_device(gm_ctx* ctx, const void* scalars_dev, const void* points_dev, siz
   if ((rc = offsets.alloc(arena, sizeof(uint32_t) * (total + 1)))) return rc;
   if ((rc = sorted.alloc(arena, sizeof(uint32_t) * (size_t)W * n))) return rc;
   if ((rc = buckets.alloc(arena, sizeof(XYZZ<DF>) * (size_t)total))) return rc;
-  if ((rc = segT.alloc(arena, sizeof(XYZZ<DF>) * (size_t)W * nseg))) return rc;
-  if ((rc = segS.alloc(arena, sizeof(XYZZ<DF>) * (size_t)W * nseg))) return rc;
-  if ((rc = wsum.alloc(arena, sizeof(uint32_t) * 4 * WORDS * W))) return rc;
+  if ((rc = nodes_a.alloc(arena, sizeof(XYZZ<DF>) * 2 * (size_t)W * nseg))) return rc;
+  if ((rc = nodes_b.alloc(arena, sizeof(XYZZ<DF>) * 2 * (size_t)W * nseg))) return rc;
+  if ((rc = wsum.alloc(arena, sizeof(uint32_t) * 4 * WORDS * W * (2 + c)))) return rc;
   const Affine<DF>* pts_internal = reinterpret_cast<const Affine<DF>*>(points_dev);
   if (!points_internal) {
     if ((rc = ipts.alloc(arena, sizeof(Affine<DF>) * n))) return rc;
@@ -415,20 +362,16 @@ int msm_device(gm_ctx* ctx, const void* scalars_dev, const void* points_dev, siz
   GM_HIP(hipGetLastError());
   int end_bit = 1;
   while ((1ull << end_bit) <= total) end_bit++;
-  size_t tmp_bytes = 0;
-  GM_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys_in.as<uint32_t>(), keys_out.as<uint32_t>(),
-                                            counts.as<uint32_t>(), sorted.as<uint32_t>(), (int)M, 0, end_bit, st));
-  if ((rc = scan_tmp.alloc(arena, tmp_bytes))) return rc;
   {
     ProfScope ps(ctx, "msm_sort");
-    GM_HIP(hipcub::DeviceRadixSort::SortPairs(scan_tmp.p, tmp_bytes, keys_in.as<uint32_t>(),
-                                              keys_out.as<uint32_t>(), counts.as<uint32_t>(),
-                                              sorted.as<uint32_t>(), (int)M, 0, end_bit, st));
+    if ((rc = msm_sort_pairs(ctx, arena, keys_in.as<uint32_t>(), keys_out.as<uint32_t>(), counts.as<uint32_t>(),
+                             sorted.as<uint32_t>(), M, end_bit)))
+      return rc;
   }
   {
     ProfScope ps(ctx, "msm_offsets");
-    hipLaunchKernelGGL(k_msm_offsets, dim3(blocks_for(M, 256)), dim3(256), 0, st, keys_out.as<uint32_t>(), M,
-                       total, offsets.as<uint32_t>());
+    hipLaunchKernelGGL(k_msm_lower_bound, dim3(blocks_for((size_t)total + 1, 256)), dim3(256), 0, st,
+                       keys_out.as<uint32_t>(), (uint32_t)M, total, offsets.as<uint32_t>());
   }
   GM_HIP(hipGetLastError());
   {
@@ -446,34 +389,65 @@ int msm_device(gm_ctx* ctx, const void* scalars_dev, const void* points_dev, siz
     hipLaunchKernelGGL(k_msm_fixup<DF>, dim3(blocks_for(total, 128)), dim3(128), 0, st, offsets.as<uint32_t>(),
                        total, K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>());
   }
+  uint32_t Q = 2;  // points per node: [G, U, Y_0..Y_{Q-3}]
   {
     ProfScope ps(ctx, "msm_bucket_reduce");
     hipLaunchKernelGGL(k_msm_seg<DF>, dim3(blocks_for((size_t)W * nseg, 128)), dim3(128), 0, st,
-                       buckets.as<XYZZ<DF>>(), nb, L, nseg, W, segT.as<XYZZ<DF>>(), segS.as<XYZZ<DF>>());
-    hipLaunchKernelGGL(k_msm_segmul<DF>, dim3(blocks_for((size_t)W * nseg, 128)), dim3(128), 0, st,
-                       segT.as<XYZZ<DF>>(), segS.as<XYZZ<DF>>(), L, nseg, W);
-    constexpr int TPB = 128;
-    hipLaunchKernelGGL((k_msm_winsum<DF, TPB>), dim3(W), dim3(TPB), sizeof(XYZZ<DF>) * TPB, st,
-                       segT.as<XYZZ<DF>>(), nseg, wsum.as<uint32_t>());
+                       buckets.as<XYZZ<DF>>(), nb, L, nseg, W, nodes_a.as<XYZZ<DF>>());
+    // LDS tree levels until one node per window
+    constexpr size_t SLOT_BUDGET = (96u << 10) / sizeof(XYZZ<DF>);
+    uint32_t m = nseg;
+    XYZZ<DF>* cur = nodes_a.as<XYZZ<DF>>();
+    XYZZ<DF>* nxt = nodes_b.as<XYZZ<DF>>();
+    while (m > 1) {
+      uint32_t lg = 0;
+      // largest power-of-two group with NT*Q slots in budget and <= 2 tasks per thread
+      while ((2u << lg) <= m && (size_t)(2u << lg) * Q <= SLOT_BUDGET && (1u << lg) * (Q + 1) <= 512) lg++;
+      if (lg == 0) {
+        set_error("msm: bucket reduction does not fit LDS");
+        return GM_ERR_INVALID;
+      }
+      const uint32_t NT = 1u << lg;
+      const uint32_t groups = m / NT;
+      hipLaunchKernelGGL(k_msm_bitsum<DF>, dim3(W * groups), dim3(256), sizeof(XYZZ<DF>) * NT * Q, st, cur, m,
+                         Q, NT, lg, nxt);
+      Q += lg;
+      m = groups;
+      std::swap(cur, nxt);
+    }
+    hipLaunchKernelGGL(k_msm_export<DF>, dim3(blocks_for((size_t)W * Q, 128)), dim3(128), 0, st, cur, W * Q,
+                       wsum.as<uint32_t>());
   }
   GM_HIP(hipGetLastError());
   uint32_t herr = 0;
   GM_HIP(hipMemcpyAsync(&herr, errw.p, 4, hipMemcpyDeviceToHost, st));
-  std::vector<HF> hw(4 * W);
+  std::vector<HF> hw(4 * (size_t)W * Q);
   static_assert(sizeof(HF) == 4 * WORDS, "host/device layout mismatch");
-  GM_HIP(hipMemcpyAsync(hw.data(), wsum.p, sizeof(uint32_t) * 4 * WORDS * W, hipMemcpyDeviceToHost, st));
+  GM_HIP(hipMemcpyAsync(hw.data(), wsum.p, sizeof(uint32_t) * 4 * WORDS * W * Q, hipMemcpyDeviceToHost, st));
   GM_HIP(hipStreamSynchronize(st));
   if (herr) {
     set_error("msm: internal consistency check failed (code " + std::to_string(herr) + ")");
     return GM_ERR_DEVICE;
   }
-  // Horner over windows
+  // Host Horner over bit positions: window w contributes U_w at 2^(c w) and
+  // Y_{w,b} at 2^(c w + log2 L + b) (b < Q - 2 = log2(nseg), so every exponent
+  // stays below c (w + 1)).
+  uint32_t lgL = 0;
+  while ((1u << lgL) < L) lgL++;
+  const int top = (int)(c * W);
+  std::vector<std::vector<uint32_t>> at(top + 1);  // point ids per exponent
+  for (uint32_t w = 0; w < W; w++) {
+    at[c * w].push_back(w * Q + 1);
+    for (uint32_t b = 0; b + 2 < Q; b++) at[c * w + lgL + b].push_back(w * Q + 2 + b);
+  }
   HJ acc = HJ::inf();
-  for (int w = (int)W - 1; w >= 0; w--) {
-    if (!acc.is_inf())
-      for (uint32_t i = 0; i < c; i++) acc = host::jdbl(acc);
-    HJ ww = host::xyzz_to_jac(hw[4 * w + 0], hw[4 * w + 1], hw[4 * w + 2], hw[4 * w + 3]);
-    acc = host::jadd(acc, ww);
+  for (int e = top; e >= 0; e--) {
+    if (!acc.is_inf()) acc = host::jdbl(acc);
+    for (uint32_t id : at[e]) {
+      const HF* p = &hw[4 * (size_t)id];
+      if (p[2].is_zero()) continue;
+      acc = host::jadd(acc, host::xyzz_to_jac(p[0], p[1], p[2], p[3]));
+    }
   }
   jac_out[0] = acc.x;
   jac_out[1] = acc.y;
@@ -496,21 +470,12 @@ int msm_prepare_points(gm_ctx* ctx, const void* gnark_points, size_t n, void* ds
   return GM_OK;
 }
 
-#define GM_MSM_PREP_INST(C, G2)                                                   \
-  template size_t msm_internal_point_bytes<C, G2>();                             \
-  template int msm_prepare_points<C, G2>(gm_ctx*, const void*, size_t, void*);
-GM_MSM_PREP_INST(CurveBN254, false)
-GM_MSM_PREP_INST(CurveBN254, true)
-GM_MSM_PREP_INST(CurveBLS12377, false)
-GM_MSM_PREP_INST(CurveBLS12377, true)
-
-template int msm_device<CurveBN254, false>(gm_ctx*, const void*, const void*, size_t,
-                                          CurveBN254::HG1F (&)[3], bool);
-template int msm_device<CurveBN254, true>(gm_ctx*, const void*, const void*, size_t,
-                                          CurveBN254::HG2F (&)[3], bool);
-template int msm_device<CurveBLS12377, false>(gm_ctx*, const void*, const void*, size_t,
-                                          CurveBLS12377::HG1F (&)[3], bool);
-template int msm_device<CurveBLS12377, true>(gm_ctx*, const void*, const void*, size_t,
-                                          CurveBLS12377::HG2F (&)[3], bool);
+// Explicit instantiation for one (curve, group); each lives in its own
+// translation unit (msm_<curve>_<group>.hip) so the four compile in parallel.
+#define GM_MSM_INSTANTIATE(C, G2)                                                              \
+  template size_t msm_internal_point_bytes<C, G2>();                                          \
+  template int msm_prepare_points<C, G2>(gm_ctx*, const void*, size_t, void*);                \
+  template int msm_device<C, G2>(gm_ctx*, const void*, const void*, size_t,                    \
+                                 typename GroupSel<C, G2>::HF (&)[3], bool);
 
 }  // namespace gm

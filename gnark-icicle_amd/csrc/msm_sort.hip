@@ -1,0 +1,23 @@
+// Radix sort of the MSM digit keys (bucket index) with their point-index
+// payloads -- the one non-templated piece of the MSM pipeline, kept in its own
+// translation unit (rocPRIM's sort is heavy to compile).
+#include <hipcub/hipcub.hpp>
+
+#include "msm.hpp"
+#include "runtime.hpp"
+
+namespace gm {
+
+int msm_sort_pairs(gm_ctx* ctx, Arena& arena, const uint32_t* keys_in, uint32_t* keys_out,
+                   const uint32_t* vals_in, uint32_t* vals_out, size_t M, int end_bit) {
+  size_t tmp_bytes = 0;
+  GM_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys_in, keys_out, vals_in, vals_out, (int)M, 0,
+                                            end_bit, ctx->stream));
+  DevBuf tmp;
+  if (int rc = tmp.alloc(arena, tmp_bytes)) return rc;
+  GM_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, tmp_bytes, keys_in, keys_out, vals_in, vals_out, (int)M, 0,
+                                            end_bit, ctx->stream));
+  return GM_OK;
+}
+
+}  // namespace gm
