@@ -41,16 +41,48 @@ GM_DEV Fe<P> ld_tab(const Fe<P>* __restrict__ t, size_t i) {
 
 GM_DEV uint32_t brev_bits(uint32_t x, int bits) { return bits ? (__brev(x) >> (32 - bits)) : 0; }
 
-// One pass.  sub: w_T^x for x < T/2 (T = 2^t); tw: pass twiddles (null if lo == 0).
+// One pass over index bits [lo, lo+t).  sub: w_T^x for x < T/2 (T = 2^t);
+// tw: inter-pass twiddles (null if lo == 0).  Fused element-wise factors, all
+// indexed by the element's global address:
+//   pb, pc  first pass only: the loaded value a becomes a*b - c (computeH PolyOps)
+//   pre     first pass only: multiply on load (coset powers)
+//   post    last pass only: multiply on store (1/n, coset^-1, 1/(g^n - 1))
+//
+// Butterfly enumeration of a stage with half-size m = 2^lm (NBF = 512 per tile):
+//  * m <= 2: twiddle-index-major, so each wave shares one twiddle index jj and the
+//    jj == 0 butterflies (twiddle 1: all of stage m = 1, half of m = 2) skip their
+//    multiplication wave-uniformly (~19% of the stage multiplications);
+//  * m >= 4: column-minor / jj-next, so consecutive lanes touch consecutive LDS
+//    elements (9-dword stride, coprime with the 64 banks: conflict-free); the
+//    jj-major order would put lanes 72m dwords apart (8- to 16-way conflicts).
+GM_DEV void bfly_index(int q, int lm, int lgB, int& jj, int& ol, int& grp) {
+  if (lm <= 1) {
+    jj = q >> (NTT_TILE_LOG - 1 - lm);
+    const int rem = q & ((NTT_TILE / 2 >> lm) - 1);
+    ol = rem & ((1 << lgB) - 1);
+    grp = rem >> lgB;
+  } else {
+    ol = q & ((1 << lgB) - 1);
+    const int k = q >> lgB;
+    jj = k & ((1 << lm) - 1);
+    grp = k >> lm;
+  }
+}
+
 template <class P, bool DIT>
 __global__ void __launch_bounds__(NTT_TPB) k_ntt_pass(Fe<P>* __restrict__ data, int logn, int lo,
                                                       int t, const Fe<P>* __restrict__ tw,
-                                                      const Fe<P>* __restrict__ sub) {
+                                                      const Fe<P>* __restrict__ sub,
+                                                      const Fe<P>* __restrict__ pre,
+                                                      const Fe<P>* __restrict__ post,
+                                                      const Fe<P>* __restrict__ pb,
+                                                      const Fe<P>* __restrict__ pc) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   Fe<P>* X = reinterpret_cast<Fe<P>*>(smem_raw);   // [T][B]
   Fe<P>* SW = X + NTT_TILE;                         // [T/2]
   const int T = 1 << t;
-  const int B = NTT_TILE >> t;
+  const int lgB = NTT_TILE_LOG - t;
+  const int B = 1 << lgB;
   const size_t nother = (size_t)1 << (logn - t);
   const size_t o0 = (size_t)blockIdx.x * B;
   const size_t lomask = ((size_t)1 << lo) - 1;
@@ -64,40 +96,46 @@ __global__ void __launch_bounds__(NTT_TPB) k_ntt_pass(Fe<P>* __restrict__ data, 
       j = q & (T - 1);
       ol = q >> t;
     } else {
-      ol = q % B;
-      j = q / B;
+      ol = q & (B - 1);
+      j = q >> lgB;
     }
     const size_t o = o0 + ol;
     if (o >= nother) continue;
     const size_t hi = o >> lo, L = o & lomask;
     const size_t addr = (hi << (lo + t)) + ((size_t)j << lo) + L;
     Fe<P> v = ld_fe(data, addr);
+    if (pb) v = fe_sub(fe_mul(v, fe_to_internal(ld_fe(pb, addr))), ld_fe(pc, addr));
+    if (pre) v = fe_mul(v, ld_tab(pre, addr));
     if (DIT && lo > 0) v = fe_mul(v, ld_tab(tw, ((size_t)j << lo) + L));
     X[j * B + ol] = v;
   }
   __syncthreads();
 
-  const int nbf = (T / 2) * B;
+  constexpr int NBF = NTT_TILE / 2;  // butterflies per stage
   if (!DIT) {
-    for (int m = T / 2; m >= 1; m >>= 1) {
-      const int step = T / (2 * m);
-      for (int q = threadIdx.x; q < nbf; q += NTT_TPB) {
-        const int ol = q % B, k = q / B;
-        const int jj = k & (m - 1), j0 = ((k / m) * 2 * m) + jj, j1 = j0 + m;
-        Fe<P> u = X[j0 * B + ol], v = X[j1 * B + ol];
+    for (int lm = t - 1; lm >= 0; lm--) {
+      const int m = 1 << lm, step = T >> (lm + 1);
+      for (int q = threadIdx.x; q < NBF; q += NTT_TPB) {
+        int jj, ol, grp;
+        bfly_index(q, lm, lgB, jj, ol, grp);
+        const int j0 = (grp << (lm + 1)) + jj, j1 = j0 + m;
+        const Fe<P> u = X[j0 * B + ol], v = X[j1 * B + ol];
         X[j0 * B + ol] = fe_add(u, v);
-        X[j1 * B + ol] = fe_mul(fe_sub(u, v), SW[jj * step]);
+        const Fe<P> d = fe_sub(u, v);
+        X[j1 * B + ol] = jj ? fe_mul(d, SW[jj * step]) : d;
       }
       __syncthreads();
     }
   } else {
-    for (int m = 1; m < T; m <<= 1) {
-      const int step = T / (2 * m);
-      for (int q = threadIdx.x; q < nbf; q += NTT_TPB) {
-        const int ol = q % B, k = q / B;
-        const int jj = k & (m - 1), j0 = ((k / m) * 2 * m) + jj, j1 = j0 + m;
-        Fe<P> u = X[j0 * B + ol];
-        Fe<P> v = fe_mul(X[j1 * B + ol], SW[jj * step]);
+    for (int lm = 0; lm < t; lm++) {
+      const int m = 1 << lm, step = T >> (lm + 1);
+      for (int q = threadIdx.x; q < NBF; q += NTT_TPB) {
+        int jj, ol, grp;
+        bfly_index(q, lm, lgB, jj, ol, grp);
+        const int j0 = (grp << (lm + 1)) + jj, j1 = j0 + m;
+        const Fe<P> u = X[j0 * B + ol];
+        Fe<P> v = X[j1 * B + ol];
+        if (jj) v = fe_mul(v, SW[jj * step]);
         X[j0 * B + ol] = fe_add(u, v);
         X[j1 * B + ol] = fe_sub(u, v);
       }
@@ -111,8 +149,8 @@ __global__ void __launch_bounds__(NTT_TPB) k_ntt_pass(Fe<P>* __restrict__ data, 
       j = q & (T - 1);
       ol = q >> t;
     } else {
-      ol = q % B;
-      j = q / B;
+      ol = q & (B - 1);
+      j = q >> lgB;
     }
     const size_t o = o0 + ol;
     if (o >= nother) continue;
@@ -120,6 +158,7 @@ __global__ void __launch_bounds__(NTT_TPB) k_ntt_pass(Fe<P>* __restrict__ data, 
     const size_t addr = (hi << (lo + t)) + ((size_t)j << lo) + L;
     Fe<P> v = X[j * B + ol];
     if (!DIT && lo > 0) v = fe_mul(v, ld_tab(tw, ((size_t)j << lo) + L));
+    if (post) v = fe_mul(v, ld_tab(post, addr));
     st_fe(data, addr, v);
   }
 }
@@ -142,15 +181,16 @@ GM_DEV Fe<P> fe_pow_u32(const Fe<P>& base, uint32_t e) {
 // tw[j*2^lo + L] = w^(L * bitrev_t(j)), w = w_{2^(lo+t)} (canonical exponent < 2^(lo+t));
 // w arrives in gnark form, tables are written in internal form.
 template <class P>
-__global__ void k_gen_pass_tw(Fe<P>* __restrict__ tw, int lo, int t, FeG<P> wg) {
+__global__ void k_gen_pass_tw(Fe<P>* __restrict__ tw, int lo, int t, FeG<P> wg, FeG<P> mult_g) {
   const Fe<P> w = fe_to_internal(fe_unpack<P>(wg));
+  const Fe<P> mult = fe_to_internal(fe_unpack<P>(mult_g));
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t size = (size_t)1 << (lo + t);
   if (i >= size) return;
   const uint32_t j = (uint32_t)(i >> lo), L = (uint32_t)(i & (((size_t)1 << lo) - 1));
   const uint64_t e = (uint64_t)L * brev_bits(j, t);
   // e < 2^(lo+t) <= 2^32 for supported sizes
-  tw[i] = fe_pow_u32(w, (uint32_t)e);
+  tw[i] = fe_mul(fe_pow_u32(w, (uint32_t)e), mult);
 }
 
 // out[x] = base^x * mult, x < count (gnark-form inputs, internal-form table)
@@ -163,16 +203,16 @@ __global__ void k_gen_powers(Fe<P>* __restrict__ out, size_t count, FeG<P> base_
   out[i] = fe_mul(fe_pow_u32(base, (uint32_t)i), mult);
 }
 
-// a[i] *= lo[e & m] * hi[e >> s], e = i or bitrev(i)
+// out[i] = mult * base^e, e = i or bitrev_logn(i) (full-size coset tables;
+// gnark-form inputs, internal-form table)
 template <class P, bool BREV>
-__global__ void __launch_bounds__(256) k_scale_pow(Fe<P>* __restrict__ a, size_t n, int logn,
-                                                   const Fe<P>* __restrict__ tlo,
-                                                   const Fe<P>* __restrict__ thi, int s) {
+__global__ void k_gen_coset(Fe<P>* __restrict__ out, size_t n, int logn, FeG<P> base_g, FeG<P> mult_g) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  const Fe<P> base = fe_to_internal(fe_unpack<P>(base_g));
+  const Fe<P> mult = fe_to_internal(fe_unpack<P>(mult_g));
   const uint32_t e = BREV ? brev_bits((uint32_t)i, logn) : (uint32_t)i;
-  Fe<P> f = fe_mul(ld_tab(tlo, e & ((1u << s) - 1)), ld_tab(thi, e >> s));
-  st_fe(a, i, fe_mul(ld_fe(a, i), f));
+  out[i] = fe_mul(fe_pow_u32(base, e), mult);
 }
 
 template <class P>
@@ -212,9 +252,13 @@ __global__ void __launch_bounds__(256) k_bitrev_swap(Fe<P>* __restrict__ a, size
 // ---------------------------------------------------------------------------
 struct NttPass {
   int lo, t;
-  void* tw_fwd;  // null if lo == 0
+  void* tw_fwd;     // null if lo == 0
   void* tw_inv;
+  void* tw_inv_ns;  // n^-1 * tw_inv (top pass only): folds the INTT scaling into a pass
 };
+
+// full-size element-wise tables (built on first use, n internal-form elements)
+enum NttTab { TAB_G_NAT, TAB_G_BREV, TAB_GI_NAT, TAB_GI_BREV, TAB_H_POST, TAB_COUNT };
 
 template <class C>
 struct NttDomain {
@@ -225,9 +269,7 @@ struct NttDomain {
   std::vector<NttPass> passes;  // DIF order (high bits first)
   void* sub_fwd[NTT_TMAX + 1] = {};
   void* sub_inv[NTT_TMAX + 1] = {};
-  // coset tables: g^x (lo/hi), n^-1 g^-x (lo/hi), size 2^s and 2^(logn - s)
-  int cs;
-  void *g_lo, *g_hi, *gi_lo, *gi_hi;
+  void* tab[TAB_COUNT] = {};
   HF omega, omega_inv, ninv, g;
   std::vector<void*> allocs;
 };
@@ -255,11 +297,18 @@ static typename NttDomain<C>::HF host_omega(int logn) {
 }
 
 template <class C>
-static int domain_alloc(NttDomain<C>* d, size_t bytes, void** out, hipStream_t st) {
-  (void)st;
+static int domain_alloc(NttDomain<C>* d, size_t bytes, void** out) {
   GM_HIP(hipMalloc(out, bytes ? bytes : 16));
   d->allocs.push_back(*out);
   return GM_OK;
+}
+
+template <class HF, class Fr>
+static FeG<Fr> to_dev(const HF& h) {
+  FeG<Fr> r;
+  static_assert(sizeof(r.w) == sizeof(h.v), "gnark layout");
+  memcpy(r.w, h.v, sizeof(r.w));
+  return r;
 }
 
 template <class C>
@@ -275,12 +324,7 @@ static int domain_build(gm_ctx* ctx, int logn, NttDomain<C>** out) {
   d->omega_inv = host::finv(d->omega);
   d->ninv = host::finv(host::from_u64<HFr>(d->n));
   d->g = host::from_u64<HFr>(C::COSET_GEN);
-  auto dev = [](const HF& h) {
-    FeG<Fr> r;
-    static_assert(sizeof(r.w) == sizeof(h.v), "gnark layout");
-    memcpy(r.w, h.v, sizeof(r.w));
-    return r;
-  };
+  auto dev = [](const HF& h) { return to_dev<HF, Fr>(h); };
   int rc;
   // pass plan
   if (logn > 0) {
@@ -293,7 +337,7 @@ static int domain_build(gm_ctx* ctx, int logn, NttDomain<C>** out) {
       ps.t = t;
       ps.lo = hi_bit - t;
       hi_bit -= t;
-      ps.tw_fwd = ps.tw_inv = nullptr;
+      ps.tw_fwd = ps.tw_inv = ps.tw_inv_ns = nullptr;
       if (ps.lo > 0) {
         size_t sz = (size_t)1 << (ps.lo + ps.t);
         // w_{N'} = omega^(n / N')
@@ -302,12 +346,18 @@ static int domain_build(gm_ctx* ctx, int logn, NttDomain<C>** out) {
           wf = wf * wf;
           wi = wi * wi;
         }
-        if ((rc = domain_alloc(d, sizeof(Fe<Fr>) * sz, &ps.tw_fwd, st))) return rc;
-        if ((rc = domain_alloc(d, sizeof(Fe<Fr>) * sz, &ps.tw_inv, st))) return rc;
+        if ((rc = domain_alloc(d, sizeof(Fe<Fr>) * sz, &ps.tw_fwd))) return rc;
+        if ((rc = domain_alloc(d, sizeof(Fe<Fr>) * sz, &ps.tw_inv))) return rc;
+        const HF one = HF::one();
         hipLaunchKernelGGL(k_gen_pass_tw<Fr>, dim3(blocks_for(sz, 256)), dim3(256), 0, st,
-                           (Fe<Fr>*)ps.tw_fwd, ps.lo, ps.t, dev(wf));
+                           (Fe<Fr>*)ps.tw_fwd, ps.lo, ps.t, dev(wf), dev(one));
         hipLaunchKernelGGL(k_gen_pass_tw<Fr>, dim3(blocks_for(sz, 256)), dim3(256), 0, st,
-                           (Fe<Fr>*)ps.tw_inv, ps.lo, ps.t, dev(wi));
+                           (Fe<Fr>*)ps.tw_inv, ps.lo, ps.t, dev(wi), dev(one));
+        if (p == 0) {
+          if ((rc = domain_alloc(d, sizeof(Fe<Fr>) * sz, &ps.tw_inv_ns))) return rc;
+          hipLaunchKernelGGL(k_gen_pass_tw<Fr>, dim3(blocks_for(sz, 256)), dim3(256), 0, st,
+                             (Fe<Fr>*)ps.tw_inv_ns, ps.lo, ps.t, dev(wi), dev(d->ninv));
+        }
       }
       d->passes.push_back(ps);
       if (!d->sub_fwd[t]) {
@@ -317,8 +367,8 @@ static int domain_build(gm_ctx* ctx, int logn, NttDomain<C>** out) {
           wi = wi * wi;
         }
         size_t cnt = (size_t)1 << (t - 1);
-        if ((rc = domain_alloc(d, sizeof(Fe<Fr>) * cnt, &d->sub_fwd[t], st))) return rc;
-        if ((rc = domain_alloc(d, sizeof(Fe<Fr>) * cnt, &d->sub_inv[t], st))) return rc;
+        if ((rc = domain_alloc(d, sizeof(Fe<Fr>) * cnt, &d->sub_fwd[t]))) return rc;
+        if ((rc = domain_alloc(d, sizeof(Fe<Fr>) * cnt, &d->sub_inv[t]))) return rc;
         HF one = HF::one();
         hipLaunchKernelGGL(k_gen_powers<Fr>, dim3(blocks_for(cnt, 256)), dim3(256), 0, st,
                            (Fe<Fr>*)d->sub_fwd[t], cnt, dev(wf), dev(one));
@@ -327,30 +377,39 @@ static int domain_build(gm_ctx* ctx, int logn, NttDomain<C>** out) {
       }
     }
   }
-  // coset tables
-  d->cs = (logn + 1) / 2;
-  size_t nlo = (size_t)1 << d->cs, nhi = (size_t)1 << (logn - d->cs);
-  HF gi = host::finv(d->g);
-  HF g_s = d->g, gi_s = gi;  // g^(2^cs)
-  for (int i = 0; i < d->cs; i++) {
-    g_s = g_s * g_s;
-    gi_s = gi_s * gi_s;
-  }
-  HF one = HF::one();
-  if ((rc = domain_alloc(d, sizeof(Fe<Fr>) * nlo, &d->g_lo, st))) return rc;
-  if ((rc = domain_alloc(d, sizeof(Fe<Fr>) * nhi, &d->g_hi, st))) return rc;
-  if ((rc = domain_alloc(d, sizeof(Fe<Fr>) * nlo, &d->gi_lo, st))) return rc;
-  if ((rc = domain_alloc(d, sizeof(Fe<Fr>) * nhi, &d->gi_hi, st))) return rc;
-  hipLaunchKernelGGL(k_gen_powers<Fr>, dim3(blocks_for(nlo, 256)), dim3(256), 0, st, (Fe<Fr>*)d->g_lo,
-                     nlo, dev(d->g), dev(one));
-  hipLaunchKernelGGL(k_gen_powers<Fr>, dim3(blocks_for(nhi, 256)), dim3(256), 0, st, (Fe<Fr>*)d->g_hi,
-                     nhi, dev(g_s), dev(one));
-  hipLaunchKernelGGL(k_gen_powers<Fr>, dim3(blocks_for(nlo, 256)), dim3(256), 0, st,
-                     (Fe<Fr>*)d->gi_lo, nlo, dev(gi), dev(d->ninv));
-  hipLaunchKernelGGL(k_gen_powers<Fr>, dim3(blocks_for(nhi, 256)), dim3(256), 0, st,
-                     (Fe<Fr>*)d->gi_hi, nhi, dev(gi_s), dev(one));
   GM_HIP(hipGetLastError());
   *out = d;
+  return GM_OK;
+}
+
+// Element-wise table `which` of the domain, built on first use:
+//   G_NAT[i] = g^i, G_BREV[i] = g^brev(i)                    (forward coset, on load)
+//   GI_NAT[i] = g^-i / n, GI_BREV[i] = g^-brev(i) / n        (inverse coset, on store)
+//   H_POST[i] = g^-brev(i) / (n (g^n - 1))                   (computeH final INTT)
+template <class C>
+static int domain_table(gm_ctx* ctx, NttDomain<C>* d, int which, const Fe<typename C::Fr>** out) {
+  using Fr = typename C::Fr;
+  using HF = typename NttDomain<C>::HF;
+  if (!d->tab[which]) {
+    int rc;
+    if ((rc = domain_alloc(d, sizeof(Fe<Fr>) * d->n, &d->tab[which]))) return rc;
+    const HF gi = host::finv(d->g);
+    HF base = d->g, mult = HF::one();
+    if (which == TAB_GI_NAT || which == TAB_GI_BREV) {
+      base = gi;
+      mult = d->ninv;
+    } else if (which == TAB_H_POST) {
+      uint64_t e[1] = {d->n};
+      base = gi;
+      mult = d->ninv * host::finv(host::fpow(d->g, e, 1) - HF::one());
+    }
+    const bool brev = which == TAB_G_BREV || which == TAB_GI_BREV || which == TAB_H_POST;
+    auto k = brev ? k_gen_coset<Fr, true> : k_gen_coset<Fr, false>;
+    hipLaunchKernelGGL(k, dim3(blocks_for(d->n, 256)), dim3(256), 0, ctx->stream, (Fe<Fr>*)d->tab[which], d->n,
+                       d->logn, to_dev<HF, Fr>(base), to_dev<HF, Fr>(mult));
+    GM_HIP(hipGetLastError());
+  }
+  *out = (const Fe<Fr>*)d->tab[which];
   return GM_OK;
 }
 
@@ -376,26 +435,67 @@ static int log2_exact(size_t n) {
   return ((size_t)1 << l) == n ? l : -1;
 }
 
+// Fused element-wise work attached to a transform (see k_ntt_pass).
+template <class Fr>
+struct NttFuse {
+  const Fe<Fr>* pre = nullptr;   // first pass, on load
+  const Fe<Fr>* post = nullptr;  // last pass, on store
+  const Fe<Fr>* pb = nullptr;    // first pass, a <- a*b - c
+  const Fe<Fr>* pc = nullptr;
+  bool scale_ninv = false;       // inverse without coset: fold 1/n into the top pass
+};
+
 template <class C>
-static int run_passes(gm_ctx* ctx, NttDomain<C>* d, Fe<typename C::Fr>* a, bool inverse, bool dit) {
+static int run_passes(gm_ctx* ctx, NttDomain<C>* d, Fe<typename C::Fr>* a, bool inverse, bool dit,
+                      const NttFuse<typename C::Fr>& fz) {
   using Fr = typename C::Fr;
   hipStream_t st = ctx->stream;
   const size_t smem = sizeof(Fe<Fr>) * (NTT_TILE + (1 << (NTT_TMAX - 1)));
   const int np = (int)d->passes.size();
   for (int k = 0; k < np; k++) {
-    const NttPass& ps = dit ? d->passes[np - 1 - k] : d->passes[k];
-    const Fe<Fr>* tw = (const Fe<Fr>*)(inverse ? ps.tw_inv : ps.tw_fwd);
+    const int pi = dit ? np - 1 - k : k;
+    const NttPass& ps = d->passes[pi];
+    const Fe<Fr>* tw = (const Fe<Fr>*)(inverse ? ((fz.scale_ninv && pi == 0) ? ps.tw_inv_ns : ps.tw_inv)
+                                               : ps.tw_fwd);
     const Fe<Fr>* sub = (const Fe<Fr>*)(inverse ? d->sub_inv[ps.t] : d->sub_fwd[ps.t]);
+    const bool first = k == 0, last = k == np - 1;
     const size_t nother = d->n >> ps.t;
     const size_t B = NTT_TILE >> ps.t;
     const unsigned grid = (unsigned)((nother + B - 1) / B);
     ProfScope pscope(ctx, "ntt_pass");
-    if (dit)
-      hipLaunchKernelGGL((k_ntt_pass<Fr, true>), dim3(grid), dim3(NTT_TPB), smem, st, a, d->logn,
-                         ps.lo, ps.t, tw, sub);
-    else
-      hipLaunchKernelGGL((k_ntt_pass<Fr, false>), dim3(grid), dim3(NTT_TPB), smem, st, a, d->logn,
-                         ps.lo, ps.t, tw, sub);
+    auto kern = dit ? k_ntt_pass<Fr, true> : k_ntt_pass<Fr, false>;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(NTT_TPB), smem, st, a, d->logn, ps.lo, ps.t, tw, sub,
+                       first ? fz.pre : nullptr, last ? fz.post : nullptr, first ? fz.pb : nullptr,
+                       first ? fz.pc : nullptr);
+  }
+  GM_HIP(hipGetLastError());
+  return GM_OK;
+}
+
+// gnark fft.Domain semantics on n = 2^logn elements, all element-wise factors
+// fused into the first / last pass.
+template <class C>
+static int transform(gm_ctx* ctx, NttDomain<C>* d, void* data, bool inverse, bool dit, bool coset,
+                     NttFuse<typename C::Fr> fz) {
+  using Fr = typename C::Fr;
+  Fe<Fr>* a = reinterpret_cast<Fe<Fr>*>(data);
+  int rc;
+  // n = 1: every mode is the identity (w = g^0 = 1, 1/n = 1)
+  if (d->logn == 0 && !fz.pb) return GM_OK;
+  if (coset) {
+    // forward: coefficient index of position p is p (DIF) or brev(p) (DIT);
+    // inverse: output position p holds coefficient p (DIT) or brev(p) (DIF)
+    const int which = inverse ? (dit ? TAB_GI_NAT : TAB_GI_BREV) : (dit ? TAB_G_BREV : TAB_G_NAT);
+    if ((rc = domain_table<C>(ctx, d, which, inverse ? &fz.post : &fz.pre))) return rc;
+  } else if (inverse && !fz.post) {
+    fz.scale_ninv = true;
+  }
+  if ((rc = run_passes<C>(ctx, d, a, inverse, dit, fz))) return rc;
+  if (fz.scale_ninv && d->passes[0].lo == 0) {
+    // single pass (logn <= NTT_TMAX): no inter-pass twiddle to fold 1/n into
+    ProfScope ps(ctx, "ntt_scale");
+    hipLaunchKernelGGL(k_scale_const<Fr>, dim3(blocks_for(d->n, 256)), dim3(256), 0, ctx->stream, a, d->n,
+                       to_dev<typename NttDomain<C>::HF, Fr>(d->ninv));
   }
   GM_HIP(hipGetLastError());
   return GM_OK;
@@ -403,7 +503,6 @@ static int run_passes(gm_ctx* ctx, NttDomain<C>* d, Fe<typename C::Fr>* a, bool 
 
 template <class C>
 int ntt_device(gm_ctx* ctx, void* data, size_t n, bool inverse, bool dit, bool coset) {
-  using Fr = typename C::Fr;
   const int logn = log2_exact(n);
   if (logn < 0 || logn > C::TWO_ADICITY || logn > 30) {
     set_error("ntt: n must be a power of two within the 2-adicity");
@@ -412,39 +511,7 @@ int ntt_device(gm_ctx* ctx, void* data, size_t n, bool inverse, bool dit, bool c
   NttDomain<C>* d;
   int rc = get_domain<C>(ctx, logn, &d);
   if (rc) return rc;
-  hipStream_t st = ctx->stream;
-  Fe<Fr>* a = reinterpret_cast<Fe<Fr>*>(data);
-  const unsigned g = blocks_for(n, 256);
-  if (!inverse) {
-    if (coset) {
-      ProfScope ps(ctx, "ntt_scale");
-      if (dit)
-        hipLaunchKernelGGL((k_scale_pow<Fr, true>), dim3(g), dim3(256), 0, st, a, n, logn,
-                           (const Fe<Fr>*)d->g_lo, (const Fe<Fr>*)d->g_hi, d->cs);
-      else
-        hipLaunchKernelGGL((k_scale_pow<Fr, false>), dim3(g), dim3(256), 0, st, a, n, logn,
-                           (const Fe<Fr>*)d->g_lo, (const Fe<Fr>*)d->g_hi, d->cs);
-    }
-    if ((rc = run_passes<C>(ctx, d, a, false, dit))) return rc;
-  } else {
-    if ((rc = run_passes<C>(ctx, d, a, true, dit))) return rc;
-    ProfScope ps(ctx, "ntt_scale");
-    if (coset) {
-      // DIF output is bit-reversed: coefficient index = bitrev(i)
-      if (dit)
-        hipLaunchKernelGGL((k_scale_pow<Fr, false>), dim3(g), dim3(256), 0, st, a, n, logn,
-                           (const Fe<Fr>*)d->gi_lo, (const Fe<Fr>*)d->gi_hi, d->cs);
-      else
-        hipLaunchKernelGGL((k_scale_pow<Fr, true>), dim3(g), dim3(256), 0, st, a, n, logn,
-                           (const Fe<Fr>*)d->gi_lo, (const Fe<Fr>*)d->gi_hi, d->cs);
-    } else {
-      FeG<Fr> k;
-      memcpy(k.w, d->ninv.v, sizeof(k.w));
-      hipLaunchKernelGGL(k_scale_const<Fr>, dim3(g), dim3(256), 0, st, a, n, k);
-    }
-  }
-  GM_HIP(hipGetLastError());
-  return GM_OK;
+  return transform<C>(ctx, d, data, inverse, dit, coset, NttFuse<typename C::Fr>());
 }
 
 template <class C>
@@ -474,30 +541,41 @@ int reverse_device(gm_ctx* ctx, void* a, size_t n) {
   return GM_OK;
 }
 
-// computeH (prove.go:356-399): INTT(DIF) -> coset NTT(DIT) for a, b, c;
-// (a*b - c) * den; coset INTT(DIF) -> h bit-reversed.
+// computeH (prove.go:356-399; icicle.go:453-513), all scalings fused:
+//   a, b, c: INTT (DIF; 1/n folded into the top-pass twiddles) -> bit-reversed
+//            coefficients -> coset NTT (DIT; g^brev(p) applied on load) -> natural
+//            evaluations on the coset g*<w>
+//   a <- a*b - c (on load of the first pass of the final transform)
+//   coset INTT (DIF) with g^-brev(p) / (n (g^n - 1)) on store -> h, bit-reversed
+//   (the order pk.G1.Z uses, setup.go:265-267; icicle.go:510 reverses explicitly)
 template <class C>
 int compute_h_device(gm_ctx* ctx, void* a, void* b, void* c, size_t len, size_t n) {
-  using HFr = typename C::HFr;
-  using HF = host::F<HFr>;
+  using Fr = typename C::Fr;
   if (len > n) {
     set_error("compute_h: len > n");
+    return GM_ERR_INVALID;
+  }
+  const int logn = log2_exact(n);
+  if (logn < 1 || logn > C::TWO_ADICITY || logn > 30) {
+    set_error("compute_h: n must be a power of two >= 2 within the 2-adicity");
     return GM_ERR_INVALID;
   }
   hipStream_t st = ctx->stream;
   if (len < n) {
     for (void* v : {a, b, c}) GM_HIP(hipMemsetAsync((char*)v + 32 * len, 0, 32 * (n - len), st));
   }
+  NttDomain<C>* d;
   int rc;
+  if ((rc = get_domain<C>(ctx, logn, &d))) return rc;
   for (void* v : {a, b, c}) {
-    if ((rc = ntt_device<C>(ctx, v, n, true, false, false))) return rc;
-    if ((rc = ntt_device<C>(ctx, v, n, false, true, true))) return rc;
+    if ((rc = transform<C>(ctx, d, v, true, false, false, NttFuse<Fr>()))) return rc;
+    if ((rc = transform<C>(ctx, d, v, false, true, true, NttFuse<Fr>()))) return rc;
   }
-  HF g = host::from_u64<HFr>(C::COSET_GEN);
-  uint64_t e[1] = {n};
-  HF den = host::finv(host::fpow(g, e, 1) - HF::one());
-  if ((rc = poly_ops_device<C>(ctx, a, b, c, n, den.v))) return rc;
-  return ntt_device<C>(ctx, a, n, true, false, true);
+  NttFuse<Fr> fz;
+  fz.pb = (const Fe<Fr>*)b;
+  fz.pc = (const Fe<Fr>*)c;
+  if ((rc = domain_table<C>(ctx, d, TAB_H_POST, &fz.post))) return rc;
+  return transform<C>(ctx, d, a, true, false, false, fz);
 }
 
 #define GM_NTT_INST(C)                                                                   \
