@@ -27,6 +27,10 @@ sys.path.insert(0, os.path.join(ROOT, "gnark-icicle_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (8.0 TB/s spec)
 MSM_BYTES_PER_POINT = 96  # 64 B affine point + 32 B scalar
+# radix-2^29 BN254 Fp (9 limbs): mul = 2*81 mads, sqr = 45 + 81; mixed add = 8M + 2S
+MADS_PER_MIXED_ADD = 8 * 162 + 2 * 126
+# measured v_mad_u64_u32 issue peak (tools/microbench/mulos.hip: 125.6 Gmul/s x 162)
+MAD_PEAK_T = 20.3
 NTT_BYTES_PER_ELEM = 64   # one 32 B read + one 32 B write per transform
 
 
@@ -37,7 +41,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--logn", type=int, default=20, help="MSM points per GPU = 2^logn")
     ap.add_argument("--ntt-logn", type=int, default=24)
-    ap.add_argument("--g16-logn", type=int, default=20, help="Groth16 prove domain (0 = skip)")
+    ap.add_argument("--g16-logn", type=str, default="20,24", help="Groth16 prove domains, comma list ('' = skip)")
+    ap.add_argument("--msm-extra", type=int, default=1, help="secondary G2 / BLS12-377 MSM lines (0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
     return ap.parse_args()
@@ -82,16 +87,9 @@ def main():
         torch.cuda.synchronize()
 
     def step():
-        jac, _ = ctx.msm("bn254", S, P, n)
         if dist is not None:
-            t = torch.frombuffer(bytearray(jac), dtype=torch.uint8).cuda()
-            parts = [torch.empty_like(t) for _ in range(world)]
-            dist.all_gather(parts, t)
-            acc = parts[0].cpu().numpy().tobytes()
-            for q in parts[1:]:
-                acc = gm.jac_add("bn254", False, acc, q.cpu().numpy().tobytes())
-            jac = acc
-        return jac
+            return gm.sharded_msm(ctx, "bn254", S, P, n, device="cuda")
+        return ctx.msm("bn254", S, P, n)[0]
 
     for _ in range(args.warmup):
         step()
@@ -118,16 +116,25 @@ def main():
     acc_avg_ms = acc_ms / max(acc_cnt, 1)
     alg_bytes = MSM_BYTES_PER_POINT * n  # per launch: one MSM of n points
     achieved_gbs = alg_bytes / (acc_avg_ms * 1e-3) / 1e9 if acc_avg_ms > 0 else 0.0
+    c = max(8, min(20, n.bit_length() - 1 - 4))   # gm choose_window
+    windows = -(-255 // c)                          # ceil((254 + 1) / c)
+    mads = n * windows * MADS_PER_MIXED_ADD         # ~one XYZZ mixed add per (point, window)
+    tmads = mads / (acc_avg_ms * 1e-3) / 1e12 if acc_avg_ms > 0 else 0.0
     roofline = {
-        "kernel": "k_msm_accum<Fe<Bn254Fp>> (msm_accum_g1)",
+        "kernel": "k_msm_accum_seg<Fe<Bn254Fp>> (msm_accum_g1)",
         "bound": "hbm",
         "achieved": round(achieved_gbs, 2),
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
         "frac": round(achieved_gbs / HBM_PEAK_GBS, 5),
-        "traffic": load_pmc_traffic("msm_accum_g1"),
+        "traffic": load_pmc_traffic("k_msm_accum_seg"),
         "avg_launch_ms": round(acc_avg_ms, 4),
-        "note": "MSM is 32-bit integer-multiply bound (no MFMA); see DESIGN.md for the int-ALU roofline",
+        "bytes_per_launch": alg_bytes,
+        "int_alu": {"achieved": round(tmads, 3), "peak": MAD_PEAK_T, "unit": "T v_mad_u64_u32/s",
+                    "frac": round(tmads / MAD_PEAK_T, 4),
+                    "work": "%d points x %d windows XYZZ mixed adds x %d mads" % (n, windows, MADS_PER_MIXED_ADD)},
+        "note": "MSM bucket accumulation is bound by 32-bit integer multiply issue (no MFMA, no HBM pressure): "
+                "int_alu is the binding roofline (DESIGN.md section 3)",
     }
     kernel_ms = {k: round(v[0] / max(v[1], 1), 4) for k, v in stats.items()}
 
@@ -186,9 +193,31 @@ def secondary(ctx, gm, args):
     res["ntt"] = {"logn": args.ntt_logn, "gelem_per_s": round(nn / dt / 1e9, 4), "ms_per_transform": round(dt * 1e3, 4),
                   "achieved_gbs": round(gbs, 1), "frac_hbm": round(gbs / HBM_PEAK_GBS, 4),
                   "avg_pass_ms": round(avg_pass, 4), "passes_per_transform": round(pass_cnt / (2 * reps), 2)}
+    if args.msm_extra:
+        res["msm"] = {}
+        for curve, g2, logn in (("bn254", True, 20), ("bls12377", False, 22), ("bls12377", True, 22)):
+            res["msm"]["%s_%s_2^%d" % (curve, "g2" if g2 else "g1", logn)] = msm_line(ctx, gm, curve, g2, logn)
     if args.g16_logn:
-        res["groth16"] = groth16_bench(ctx, gm, args.g16_logn)
+        res["groth16"] = [groth16_bench(ctx, gm, int(l)) for l in args.g16_logn.split(",") if l]
     return res
+
+
+def msm_line(ctx, gm, curve, g2, logn, reps=5):
+    """Mpoints/s of one more MSM configuration (BASELINE configs[4]: BLS12-377 G1+G2 2^22)."""
+    n = 1 << logn
+    S = ctx.random_scalars(curve, n, 0x5EED0005)
+    K = ctx.random_scalars(curve, n, 0x5EED1005)
+    P = ctx.batch_mul_base(curve, g2, gm.generator(curve, g2), K, n)
+    K.free()
+    ctx.msm(curve, S, P, n, g2=g2)
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ctx.msm(curve, S, P, n, g2=g2)
+    dt = (time.perf_counter() - t0) / reps
+    S.free()
+    P.free()
+    return {"mpoints_per_s": round(n / dt / 1e6, 3), "ms": round(dt * 1e3, 3)}
 
 
 def groth16_bench(ctx, gm, logn):
@@ -221,9 +250,9 @@ def groth16_bench(ctx, gm, logn):
     srcs = [ctx.random_scalars("bn254", n, 9 + i) for i in range(3)]
     r = ctx.random_scalars("bn254", 2, 12).to_host()
     times = []
-    for it in range(3):
+    for it in range(3 if logn < 24 else 2):
         for dst, src in zip((A, B, C), srcs):
-            dst.write(src.to_host())
+            dst.copy_from(src)
         ctx.synchronize()
         t0 = time.perf_counter()
         dpk.prove_device(W, A, B, C, n, r[:32], r[32:])

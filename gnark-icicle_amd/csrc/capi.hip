@@ -263,6 +263,13 @@ int gm_memcpy_d2h(gm_ctx* ctx, void* host, const void* dev, size_t bytes) {
   GM_HIP(hipStreamSynchronize(ctx->stream));
   return GM_OK;
 }
+int gm_memcpy_d2d(gm_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  GM_HIP(hipSetDevice(ctx->device));
+  GM_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+  GM_HIP(hipStreamSynchronize(ctx->stream));
+  return GM_OK;
+}
 int gm_copy_to_device(gm_ctx* ctx, const void* host, size_t bytes, void** dev_out) {
   int rc = gm_malloc(ctx, bytes, dev_out);
   if (rc) return rc;
@@ -509,7 +516,15 @@ int gm_g16_pk_upload(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, gm_g16_pk*
     if (!h->infA[i]) ia.push_back((uint32_t)i);
     if (!h->infB[i]) ib.push_back((uint32_t)i);
   }
-  for (size_t i = 0; i < pk->nbK; i++) ik.push_back((uint32_t)(pk->nb_public + i));
+  for (size_t i = 0; i < pk->nbK; i++) {
+    const size_t w = h->k_wires ? (size_t)h->k_wires[i] : pk->nb_public + i;
+    if (w >= pk->nb_wires || w < pk->nb_public) {
+      set_error("pk upload: K wire index out of range");
+      delete pk;
+      return GM_ERR_INVALID;
+    }
+    ik.push_back((uint32_t)w);
+  }
   if (ia.size() != pk->nbA || ib.size() != pk->nbB || pk->nb_public + pk->nbK > pk->nb_wires) {
     set_error("pk upload: infinity masks inconsistent with nbA/nbB/nbK");
     delete pk;

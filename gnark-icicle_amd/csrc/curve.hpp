@@ -161,6 +161,21 @@ GM_DEV Affine<F> load_affine_gnark(const uint32_t* __restrict__ src) {
   r.y = Coord<F>::load_internal(src + Coord<F>::WORDS);
   return r;
 }
+// Affine point in "packed internal" layout (see Coord::load_packed): the MSM's
+// resident point format -- gnark's size (64 B for BN254 G1, 128-B lines hold two
+// points, no point straddles a 64-B sector) with no per-load conversion multiply.
+template <class F>
+GM_DEV Affine<F> load_affine_packed(const uint32_t* __restrict__ src) {
+  Affine<F> r;
+  r.x = Coord<F>::load_packed(src);
+  r.y = Coord<F>::load_packed(src + Coord<F>::WORDS);
+  return r;
+}
+template <class F>
+GM_DEV void store_affine_packed(uint32_t* __restrict__ dst, const Affine<F>& a) {
+  Coord<F>::store_packed(dst, a.x);
+  Coord<F>::store_packed(dst + Coord<F>::WORDS, a.y);
+}
 template <class F>
 GM_DEV void store_affine_gnark(uint32_t* __restrict__ dst, const Affine<F>& a) {
   Coord<F>::store_gnark(dst, a.x);

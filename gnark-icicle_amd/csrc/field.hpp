@@ -434,6 +434,10 @@ struct Coord<Fe<P>> {
   static constexpr int WORDS = P::NG;  // u32 words in gnark layout
   GM_DEV static Fe<P> load_internal(const uint32_t* src) { return fe_to_internal(fe_unpack<P>(feg_load<P>(src))); }
   GM_DEV static void store_gnark(uint32_t* dst, const Fe<P>& a) { feg_store<P>(dst, fe_pack(fe_to_gnark(a))); }
+  // "packed internal": the internal (x * 2^(29N) mod p) value in gnark's word
+  // layout -- same byte size as gnark, no multiplication to convert.
+  GM_DEV static Fe<P> load_packed(const uint32_t* src) { return fe_unpack<P>(feg_load<P>(src)); }
+  GM_DEV static void store_packed(uint32_t* dst, const Fe<P>& a) { feg_store<P>(dst, fe_pack(a)); }
 };
 template <class P, int B>
 struct Coord<Fe2<P, B>> {
@@ -444,6 +448,13 @@ struct Coord<Fe2<P, B>> {
   GM_DEV static void store_gnark(uint32_t* dst, const Fe2<P, B>& a) {
     Coord<Fe<P>>::store_gnark(dst, a.a0);
     Coord<Fe<P>>::store_gnark(dst + P::NG, a.a1);
+  }
+  GM_DEV static Fe2<P, B> load_packed(const uint32_t* src) {
+    return {Coord<Fe<P>>::load_packed(src), Coord<Fe<P>>::load_packed(src + P::NG)};
+  }
+  GM_DEV static void store_packed(uint32_t* dst, const Fe2<P, B>& a) {
+    Coord<Fe<P>>::store_packed(dst, a.a0);
+    Coord<Fe<P>>::store_packed(dst + P::NG, a.a1);
   }
 };
 

@@ -81,10 +81,31 @@ __global__ void __launch_bounds__(256) k_msm_keys(const uint32_t* __restrict__ s
 // ---------------------------------------------------------------------------
 template <class F>
 __global__ void __launch_bounds__(256) k_msm_convert_points(const uint32_t* __restrict__ src, size_t n,
-                                                            Affine<F>* __restrict__ dst) {
+                                                            uint32_t* __restrict__ dst) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  dst[i] = load_affine_gnark<F>(src + i * 2 * Coord<F>::WORDS);
+  constexpr int PW = 2 * Coord<F>::WORDS;
+  store_affine_packed<F>(dst + i * PW, load_affine_gnark<F>(src + i * PW));
+}
+
+// raw words of one packed point (vector loads; unpacked just before use)
+template <int PW>
+struct PackedPt {
+  uint32_t w[PW];
+};
+template <int PW>
+GM_DEV PackedPt<PW> load_packed_pt(const uint32_t* __restrict__ src) {
+  static_assert(PW % 4 == 0, "packed points are whole 16-byte chunks");
+  PackedPt<PW> r;
+#pragma unroll
+  for (int q = 0; q < PW / 4; q++) {
+    const uint4 v = reinterpret_cast<const uint4*>(src)[q];
+    r.w[4 * q] = v.x;
+    r.w[4 * q + 1] = v.y;
+    r.w[4 * q + 2] = v.z;
+    r.w[4 * q + 3] = v.w;
+  }
+  return r;
 }
 
 // Load-balanced accumulation over the sorted entry list: thread t owns entries
@@ -108,7 +129,7 @@ GM_DEV void accum_emit(uint32_t b, const XYZZ<F>& acc, bool is_first, bool is_la
 }
 
 template <class F>
-__global__ void __launch_bounds__(128) k_msm_accum_seg(const Affine<F>* __restrict__ points, uint32_t n,
+__global__ void __launch_bounds__(128) k_msm_accum_seg(const uint32_t* __restrict__ points, uint32_t n,
                                                        const uint32_t* __restrict__ keys,
                                                        const uint32_t* __restrict__ vals,
                                                        const uint32_t* __restrict__ offsets, uint32_t total,
@@ -130,12 +151,13 @@ __global__ void __launch_bounds__(128) k_msm_accum_seg(const Affine<F>* __restri
     atomicOr(err, 2u);
     return;
   }
-  Affine<F> P = points[idx];
+  constexpr int PW = 2 * Coord<F>::WORDS;  // u32 words per packed point
+  PackedPt<PW> P = load_packed_pt<PW>(points + (size_t)idx * PW);
   for (uint32_t q = start; q < end; q++) {
     const uint32_t k = keys[q];
-    // prefetch the next point while this add runs
+    // prefetch the next point's words while this add runs
     uint32_t vn = 0;
-    Affine<F> Pn;
+    PackedPt<PW> Pn;
     if (q + 1 < end) {
       vn = vals[q + 1];
       const uint32_t in = vn & 0x7fffffffu;
@@ -143,7 +165,7 @@ __global__ void __launch_bounds__(128) k_msm_accum_seg(const Affine<F>* __restri
         atomicOr(err, 2u);
         return;
       }
-      Pn = points[in];
+      Pn = load_packed_pt<PW>(points + (size_t)in * PW);
     }
     if (k != cur) {
       accum_emit(cur, acc, first, false, start, end, t, offsets, buckets, part_first, part_last);
@@ -151,30 +173,72 @@ __global__ void __launch_bounds__(128) k_msm_accum_seg(const Affine<F>* __restri
       acc = xyzz_inf<F>();
       cur = k;
     }
-    if (v >> 31) P.y = fe_neg(P.y);
-    xyzz_add_aff(acc, P);
+    Affine<F> A = load_affine_packed<F>(P.w);
+    if (v >> 31) A.y = fe_neg(A.y);
+    xyzz_add_aff(acc, A);
     v = vn;
     P = Pn;
   }
   accum_emit(cur, acc, first, true, start, end, t, offsets, buckets, part_first, part_last);
 }
 
-// Merge the partial sums of buckets cut by slice edges (bucket b spans slices t0..t1).
+// Merge the partial sums of buckets cut by slice edges.  Bucket b spans slices
+// t0..t1 and its sum is part_last[t0] + part_first[t0+1] + ... + part_first[t1].
+// Spans up to FIX_SERIAL slices are summed by one thread; longer spans (a huge
+// bucket: skewed witness values, or the nearly empty top window of a scalar
+// field much narrower than W*c bits) are tree-reduced in place over part_first
+// by k_msm_fix_tree levels -- depth log2(span) adds instead of span serial adds.
+constexpr uint32_t FIX_SERIAL = 8;
+
 template <class F>
 __global__ void __launch_bounds__(128) k_msm_fixup(const uint32_t* __restrict__ offsets, uint32_t total,
                                                    uint32_t K, XYZZ<F>* __restrict__ buckets,
                                                    const XYZZ<F>* __restrict__ part_first,
-                                                   const XYZZ<F>* __restrict__ part_last) {
+                                                   const XYZZ<F>* __restrict__ part_last,
+                                                   uint32_t* __restrict__ maxspan) {
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= total) return;
   const uint32_t bs = offsets[b], be = offsets[b + 1];
   if (be == bs) return;
   const uint32_t t0 = bs / K, t1 = (be - 1) / K;
   if (t0 == t1) return;
+  if (t1 - t0 > FIX_SERIAL) {
+    atomicMax(maxspan, t1 - t0);
+    return;
+  }
   XYZZ<F> acc = part_last[t0];
-  for (uint32_t t = t0 + 1; t < t1; t++) acc = xyzz_add(acc, part_first[t]);
-  acc = xyzz_add(acc, part_first[t1]);
+  for (uint32_t t = t0 + 1; t <= t1; t++) acc = xyzz_add(acc, part_first[t]);
   buckets[b] = acc;
+}
+
+// One level d of the pairwise tree over part_first[t0+1 .. t1] of every long span.
+template <class F>
+__global__ void __launch_bounds__(128) k_msm_fix_tree(const uint32_t* __restrict__ keys,
+                                                      const uint32_t* __restrict__ offsets, uint32_t total,
+                                                      uint32_t K, uint32_t nslices, uint32_t d,
+                                                      XYZZ<F>* __restrict__ part_first) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nslices || (size_t)t * K >= offsets[total]) return;
+  const uint32_t b = keys[(size_t)t * K];
+  const uint32_t t0 = offsets[b] / K, t1 = (offsets[b + 1] - 1) / K;
+  if (t1 - t0 <= FIX_SERIAL || t <= t0) return;
+  const uint32_t rel = t - (t0 + 1), len = t1 - t0, step = 1u << d;
+  if ((rel & ((step << 1) - 1)) == 0 && rel + step < len)
+    part_first[t] = xyzz_add(part_first[t], part_first[t + step]);
+}
+
+template <class F>
+__global__ void __launch_bounds__(128) k_msm_fixup_long(const uint32_t* __restrict__ offsets, uint32_t total,
+                                                        uint32_t K, XYZZ<F>* __restrict__ buckets,
+                                                        const XYZZ<F>* __restrict__ part_first,
+                                                        const XYZZ<F>* __restrict__ part_last) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= total) return;
+  const uint32_t bs = offsets[b], be = offsets[b + 1];
+  if (be == bs) return;
+  const uint32_t t0 = bs / K, t1 = (be - 1) / K;
+  if (t1 - t0 <= FIX_SERIAL) return;
+  buckets[b] = xyzz_add(part_last[t0], part_first[t0 + 1]);
 }
 
 // ---------------------------------------------------------------------------
@@ -289,13 +353,22 @@ static __global__ void __launch_bounds__(256) k_msm_lower_bound(const uint32_t* 
 // ---------------------------------------------------------------------------
 // host driver
 // ---------------------------------------------------------------------------
-static int choose_window(size_t n) {
-  int lg = 0;
-  while ((size_t(1) << (lg + 1)) <= n) lg++;
-  int c = lg - 4;
-  if (c < 8) c = 8;
-  if (c > 20) c = 20;
-  return c;
+// Window size minimising a cost model in EC adds: n*W accumulation adds plus
+// ~3 adds per bucket in the reduction (W*2^(c-1) buckets), W = ceil((bits+1)/c).
+// Picks c = 16 for 2^20 BN254 points, 20 for 2^24, and c = 17 (W = 15, a full top
+// window) instead of 18 for 2^22 BLS12-377 points.
+static int choose_window(size_t n, int bits) {
+  int best = 8;
+  double best_cost = 1e300;
+  for (int c = 8; c <= 20; c++) {
+    const double W = (double)((bits + 1 + c - 1) / c);
+    const double cost = (double)n * W + 3.0 * W * (double)(1u << (c - 1));
+    if (cost < best_cost) {
+      best_cost = cost;
+      best = c;
+    }
+  }
+  return best;
 }
 
 template <class C, bool G2>
@@ -316,7 +389,7 @@ int msm_device(gm_ctx* ctx, const void* scalars_dev, const void* points_dev, siz
     set_error("msm: n must be < 2^31");
     return GM_ERR_INVALID;
   }
-  const uint32_t c = ctx->msm_c_override ? (uint32_t)ctx->msm_c_override : (uint32_t)choose_window(n);
+  const uint32_t c = ctx->msm_c_override ? (uint32_t)ctx->msm_c_override : (uint32_t)choose_window(n, C::FR_BITS);
   const uint32_t W = (C::FR_BITS + 1 + c - 1) / c;  // ceil((bits+1)/c): top signed digit never carries
   const uint32_t nb = 1u << (c - 1);
   const uint32_t total = W * nb;
@@ -339,13 +412,14 @@ int msm_device(gm_ctx* ctx, const void* scalars_dev, const void* points_dev, siz
   if ((rc = nodes_a.alloc(arena, sizeof(XYZZ<DF>) * 2 * (size_t)W * nseg))) return rc;
   if ((rc = nodes_b.alloc(arena, sizeof(XYZZ<DF>) * 2 * (size_t)W * nseg))) return rc;
   if ((rc = wsum.alloc(arena, sizeof(uint32_t) * 4 * WORDS * W * (2 + c)))) return rc;
-  const Affine<DF>* pts_internal = reinterpret_cast<const Affine<DF>*>(points_dev);
+  constexpr size_t PTB = 2 * WORDS * sizeof(uint32_t);  // packed point bytes
+  const uint32_t* pts_internal = reinterpret_cast<const uint32_t*>(points_dev);
   if (!points_internal) {
-    if ((rc = ipts.alloc(arena, sizeof(Affine<DF>) * n))) return rc;
+    if ((rc = ipts.alloc(arena, PTB * n))) return rc;
     ProfScope ps(ctx, "msm_convert_points");
     hipLaunchKernelGGL(k_msm_convert_points<DF>, dim3(blocks_for(n, 256)), dim3(256), 0, st,
-                       reinterpret_cast<const uint32_t*>(points_dev), n, ipts.as<Affine<DF>>());
-    pts_internal = ipts.as<Affine<DF>>();
+                       reinterpret_cast<const uint32_t*>(points_dev), n, ipts.as<uint32_t>());
+    pts_internal = ipts.as<uint32_t>();
   }
 
   const uint32_t* sc = reinterpret_cast<const uint32_t*>(scalars_dev);
@@ -387,7 +461,20 @@ int msm_device(gm_ctx* ctx, const void* scalars_dev, const void* points_dev, siz
                        K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>(),
                        errw.as<uint32_t>());
     hipLaunchKernelGGL(k_msm_fixup<DF>, dim3(blocks_for(total, 128)), dim3(128), 0, st, offsets.as<uint32_t>(),
-                       total, K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>());
+                       total, K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>(),
+                       errw.as<uint32_t>() + 1);
+    uint32_t maxspan = 0;
+    GM_HIP(hipMemcpyAsync(&maxspan, errw.as<uint32_t>() + 1, 4, hipMemcpyDeviceToHost, st));
+    GM_HIP(hipStreamSynchronize(st));
+    if (maxspan > FIX_SERIAL) {
+      for (uint32_t d = 0; (1u << d) < maxspan; d++)
+        hipLaunchKernelGGL(k_msm_fix_tree<DF>, dim3(blocks_for(nslices, 128)), dim3(128), 0, st,
+                           keys_out.as<uint32_t>(), offsets.as<uint32_t>(), total, K, (uint32_t)nslices, d,
+                           pfirst.as<XYZZ<DF>>());
+      hipLaunchKernelGGL(k_msm_fixup_long<DF>, dim3(blocks_for(total, 128)), dim3(128), 0, st,
+                         offsets.as<uint32_t>(), total, K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(),
+                         plast.as<XYZZ<DF>>());
+    }
   }
   uint32_t Q = 2;  // points per node: [G, U, Y_0..Y_{Q-3}]
   {
@@ -457,7 +544,7 @@ int msm_device(gm_ctx* ctx, const void* scalars_dev, const void* points_dev, siz
 
 template <class C, bool G2>
 size_t msm_internal_point_bytes() {
-  return sizeof(Affine<typename GroupSel<C, G2>::DF>);
+  return 2 * Coord<typename GroupSel<C, G2>::DF>::WORDS * sizeof(uint32_t);
 }
 
 template <class C, bool G2>
@@ -465,7 +552,7 @@ int msm_prepare_points(gm_ctx* ctx, const void* gnark_points, size_t n, void* ds
   using DF = typename GroupSel<C, G2>::DF;
   if (n == 0) return GM_OK;
   hipLaunchKernelGGL(k_msm_convert_points<DF>, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream,
-                     reinterpret_cast<const uint32_t*>(gnark_points), n, reinterpret_cast<Affine<DF>*>(dst));
+                     reinterpret_cast<const uint32_t*>(gnark_points), n, reinterpret_cast<uint32_t*>(dst));
   GM_HIP(hipGetLastError());
   return GM_OK;
 }

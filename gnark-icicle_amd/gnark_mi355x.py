@@ -40,7 +40,7 @@ SYMBOLS = [
     "gm_last_error", "gm_version", "gm_init", "gm_destroy", "gm_synchronize",
     "gm_profile_enable", "gm_profile_reset", "gm_profile_get", "gm_profile_dump",
     "gm_set_msm_window", "gm_malloc", "gm_free", "gm_copy_to_device", "gm_memcpy_h2d",
-    "gm_memcpy_d2h", "gm_copy_points_to_device", "gm_msm", "gm_msm_host_scalars", "gm_ntt",
+    "gm_memcpy_d2h", "gm_memcpy_d2d", "gm_copy_points_to_device", "gm_msm", "gm_msm_host_scalars", "gm_ntt",
     "gm_poly_ops", "gm_reverse_scalars", "gm_groth16_compute_h", "gm_g16_pk_upload",
     "gm_g16_pk_free", "gm_g16_prove", "gm_g16_prove_device", "gm_jac_add", "gm_jac_to_affine",
     "gm_batch_mul_base", "gm_random_scalars", "gm_generator", "gm_test_field_op",
@@ -79,6 +79,7 @@ def load_library(path: str = LIB_PATH):
     L.gm_copy_to_device.argtypes = [vp, vp, sz, pvp]
     L.gm_memcpy_h2d.argtypes = [vp, vp, vp, sz]
     L.gm_memcpy_d2h.argtypes = [vp, vp, vp, sz]
+    L.gm_memcpy_d2d.argtypes = [vp, vp, vp, sz]
     L.gm_copy_points_to_device.argtypes = [vp, i, i, vp, sz, pvp]
     L.gm_msm.argtypes = [vp, i, i, vp, vp, sz, vp, vp]
     L.gm_msm_host_scalars.argtypes = [vp, i, i, vp, vp, sz, vp, vp]
@@ -163,6 +164,10 @@ class DeviceBuffer:
     def write(self, data, offset: int = 0):
         a = _buf(data)
         _check(load_library().gm_memcpy_h2d(self.ctx.handle, self.ptr + offset, _p(a), a.size))
+
+    def copy_from(self, src: "DeviceBuffer", nbytes: int | None = None):
+        n = min(self.nbytes, src.nbytes) if nbytes is None else nbytes
+        _check(load_library().gm_memcpy_d2d(self.ctx.handle, self.ptr, src.ptr, n))
 
     def free(self):
         if self.ptr:
@@ -319,12 +324,88 @@ class Context:
 
 
 # ---------------------------------------------------------------------------
+# Multi-GPU MSM sharding (SURVEY.md §8e): one process per GPU, each rank owns a
+# contiguous slice of the point / scalar arrays, computes its partial Pippenger
+# sum, and the N partial Jacobians (96 B G1 / 192 B G2 for BN254) are
+# all-gathered (RCCL over xGMI with backend "nccl", or gloo on CPU) and reduced
+# by N-1 host EC adds.  No other data-path communication.
+# ---------------------------------------------------------------------------
+def shard_range(n: int, world: int, rank: int) -> tuple[int, int]:
+    """[lo, hi) of the contiguous shard of n items owned by `rank` (the first
+    n % world ranks hold one extra item; a shard may be empty)."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError("bad rank/world")
+    q, r = divmod(n, world)
+    lo = rank * q + min(rank, r)
+    return lo, lo + q + (1 if rank < r else 0)
+
+
+def jac_infinity(curve, g2: bool) -> bytes:
+    """gnark's G1Jac/G2Jac point at infinity {X: 1, Y: 1, Z: 0} (Montgomery one)."""
+    out = np.zeros(jac_bytes(curve, g2), np.uint8)
+    one = _mont_one(curve, g2)
+    out[:one.size] = one
+    out[one.size:2 * one.size] = one
+    return out.tobytes()
+
+
+_MONT_ONE_CACHE: dict = {}
+
+
+def _mont_one(curve, g2: bool) -> np.ndarray:
+    """Montgomery encoding of 1 in Fp (or Fp2 = (1, 0)), gnark layout."""
+    key = (curve_id(curve), g2)
+    if key not in _MONT_ONE_CACHE:
+        cid = curve_id(curve)
+        p = {BN254: 21888242871839275222246405745257275088696311157297823662689037894645226208583,
+             BLS12_377: 258664426012969094010652733694893533536393512754914660539884262666720468348340822774968888139573360124440321458177}[cid]
+        nb = FP_BYTES[cid]
+        r = (1 << (8 * nb)) % p
+        v = np.frombuffer(r.to_bytes(nb, "little"), np.uint8)
+        if g2:
+            v = np.concatenate([v, np.zeros(nb, np.uint8)])
+        _MONT_ONE_CACHE[key] = v
+    return _MONT_ONE_CACHE[key]
+
+
+def reduce_partials(curve, g2: bool, partials) -> bytes:
+    """Sum of gnark Jacobian partial results (host EC adds)."""
+    acc = None
+    for p in partials:
+        acc = bytes(p) if acc is None else jac_add(curve, g2, acc, p)
+    return acc if acc is not None else jac_infinity(curve, g2)
+
+
+def allgather_partial(local_jac: bytes, group=None, device=None) -> list:
+    """All-gathers one Jacobian partial (fixed size) from every rank."""
+    import torch
+    import torch.distributed as dist
+    dev = device if device is not None else ("cuda" if dist.get_backend(group) == "nccl" else "cpu")
+    t = torch.frombuffer(bytearray(local_jac), dtype=torch.uint8).to(dev)
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(parts, t, group=group)
+    return [q.cpu().numpy().tobytes() for q in parts]
+
+
+def sharded_msm(ctx: "Context", curve, scalars, points, n_local: int, g2: bool = False, group=None,
+                device=None) -> bytes:
+    """Full MSM over the union of every rank's shard: local Pippenger on this
+    rank's GPU, one all-gather of the partial sums, host reduction.  Returns the
+    gnark Jacobian bytes (identical on every rank)."""
+    if n_local:
+        local = ctx.msm(curve, scalars, points, n_local, g2=g2)[0]
+    else:
+        local = jac_infinity(curve, g2)
+    return reduce_partials(curve, g2, allgather_partial(local, group=group, device=device))
+
+
+# ---------------------------------------------------------------------------
 # Groth16 (icicle_bn254 ProvingKey / Prove mirror)
 # ---------------------------------------------------------------------------
 class _PkHost(ctypes.Structure):
     _fields_ = [(k, ctypes.c_size_t) for k in ["domain_size", "nb_wires", "nb_public", "nbA", "nbB", "nbK"]] + \
                [(k, ctypes.c_void_p) for k in ["g1_alpha", "g1_beta", "g1_delta", "g1_A", "g1_B", "g1_Z", "g1_K",
-                                                "g2_beta", "g2_delta", "g2_B", "infA", "infB"]]
+                                                "g2_beta", "g2_delta", "g2_B", "infA", "infB", "k_wires"]]
 
 
 class ProvingKey:
@@ -332,14 +413,16 @@ class ProvingKey:
     provingkey.go:10-28; uploaded once like setupDevicePointers, icicle.go:31-130).
 
     `pk` is a dict of gnark-layout byte arrays: g1_alpha, g1_beta, g1_delta, g1_A,
-    g1_B, g1_Z (n-1, bit-reversed), g1_K, g2_beta, g2_delta, g2_B, infA, infB.
+    g1_B, g1_Z (n-1, bit-reversed), g1_K, g2_beta, g2_delta, g2_B, infA, infB, and
+    optionally k_wires (the wire index of each pk.G1.K point when BSB22
+    commitments filter K, prove.go:243-245; default nb_public + i).
     """
 
     def __init__(self, ctx: Context, curve, pk: dict, domain_size: int, nb_wires: int, nb_public: int):
         self.ctx = ctx
         self.curve = curve_id(curve)
         g1b = point_bytes(curve, False)
-        arrs = {k: _buf(v) for k, v in pk.items() if k != "sizes"}
+        arrs = {k: _buf(v) for k, v in pk.items() if k not in ("sizes", "k_wires")}
         h = _PkHost()
         h.domain_size, h.nb_wires, h.nb_public = domain_size, nb_wires, nb_public
         h.nbA = arrs["g1_A"].size // g1b
@@ -348,6 +431,11 @@ class ProvingKey:
         for k in ["g1_alpha", "g1_beta", "g1_delta", "g1_A", "g1_B", "g1_Z", "g1_K", "g2_beta", "g2_delta",
                   "g2_B", "infA", "infB"]:
             setattr(h, k, arrs[k].ctypes.data)
+        if "k_wires" in pk and pk["k_wires"] is not None:
+            kw = np.ascontiguousarray(np.asarray(pk["k_wires"], dtype=np.uint32))
+            h.nbK = kw.size
+            h.k_wires = kw.ctypes.data
+            arrs["k_wires"] = kw
         self._keep = arrs
         handle = ctypes.c_void_p()
         _check(load_library().gm_g16_pk_upload(ctx.handle, self.curve, ctypes.byref(h), ctypes.byref(handle)))

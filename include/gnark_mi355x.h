@@ -66,6 +66,7 @@ int gm_free(gm_ctx* ctx, void* dev);
 int gm_copy_to_device(gm_ctx* ctx, const void* host, size_t bytes, void** dev_out);
 int gm_memcpy_h2d(gm_ctx* ctx, void* dev, const void* host, size_t bytes);
 int gm_memcpy_d2h(gm_ctx* ctx, void* host, const void* dev, size_t bytes);
+int gm_memcpy_d2d(gm_ctx* ctx, void* dst_dev, const void* src_dev, size_t bytes);
 /* Uploads n gnark affine points of (curve, g2) -> device buffer. */
 int gm_copy_points_to_device(gm_ctx* ctx, int curve, int g2, const void* host_points, size_t n,
                              void** dev_out);
@@ -133,6 +134,10 @@ typedef struct {
   const void* g2_B;        /* nbB points */
   const uint8_t* infA;     /* nb_wires flags (InfinityA) */
   const uint8_t* infB;     /* nb_wires flags (InfinityB) */
+  /* nbK wire indices whose values multiply pk.G1.K: wireValues[nb_public:]
+   * minus the private-committed and commitment wires (prove.go:243-245,
+   * filterHeap :331-354).  NULL = no commitments: nb_public + i. */
+  const uint32_t* k_wires;
 } gm_g16_pk_host;
 
 int gm_g16_pk_upload(gm_ctx* ctx, int curve, const gm_g16_pk_host* pk, gm_g16_pk** out);

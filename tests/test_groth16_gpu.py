@@ -63,3 +63,39 @@ def test_groth16_rejects_bad_witness(gm_ctx, oracle):
     exp, got, ok = _prove_both(gm_ctx, oracle, "bn254", r1, W, 5, 7)
     assert got == exp  # same (invalid) computation on both sides
     assert ok != 7
+
+
+def test_groth16_k_wire_filter(gm_ctx, oracle):
+    """BSB22-style K filter (prove.go:243-245): wires removed from the K MSM are
+    given by the k_wires index map of the device pk.  Expected: the oracle prover
+    on the full pk with the removed wires' K points set to infinity (so they
+    contribute nothing)."""
+    import numpy as np
+    import gnark_mi355x as gm
+    cname = "bn254"
+    c = pyref.CURVES[cname]
+    r1, W = R.squaring_chain(200, cname, x=3)
+    tox = R.encode_vec(cname, [t % c.r for t in TOXIC])
+    pk = oracle.g16_setup(cname, r1, tox)
+    enc = lambda v: R.encode_vec(cname, v)
+    a, b, cc = r1.solve_abc(W)
+    rb, sb = enc([11]), enc([13])
+    nbk = r1.nb_wires - r1.nb_public
+    drop = {3, 17, 18, 150}
+    keep = [i for i in range(nbk) if i not in drop]
+    g1b = gm.point_bytes(cname, False)
+    K = np.frombuffer(pk["g1_K"], np.uint8).reshape(nbk, g1b)
+    pk_inf = dict(pk)
+    Kz = K.copy()
+    Kz[sorted(drop)] = 0
+    pk_inf["g1_K"] = Kz.reshape(-1)
+    exp = oracle.g16_prove(cname, pk_inf, r1.nb_public, enc(W), enc(a), enc(b), enc(cc), rb, sb)
+    pk_sub = dict(pk)
+    pk_sub["g1_K"] = K[keep].reshape(-1)
+    pk_sub["k_wires"] = [r1.nb_public + i for i in keep]
+    dpk = gm.ProvingKey(gm_ctx, cname, pk_sub, r1.domain_size, r1.nb_wires, r1.nb_public)
+    try:
+        got = dpk.prove(enc(W), enc(a), enc(b), enc(cc), rb, sb)
+    finally:
+        dpk.free()
+    assert got == exp
