@@ -311,6 +311,87 @@ int gm_msm_host_scalars(gm_ctx* ctx, int curve, int g2, const void* scalars_host
   return gm_msm(ctx, curve, g2, s.p, points_dev, n, out_jac, out_affine);
 }
 
+int gm_points_upload(gm_ctx* ctx, int curve, int g2, const void* host_points, size_t n, void** out) {
+  if (!ctx || !out) return GM_ERR_INVALID;
+  if (int rc = check_curve(curve)) return rc;
+  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  GM_HIP(hipSetDevice(ctx->device));
+  const size_t gb = fp_bytes(curve) * (g2 ? 4 : 2) * n;
+  const size_t ib = n * (curve == GM_BN254 ? (g2 ? msm_internal_point_bytes<CurveBN254, true>()
+                                                 : msm_internal_point_bytes<CurveBN254, false>())
+                                           : (g2 ? msm_internal_point_bytes<CurveBLS12377, true>()
+                                                 : msm_internal_point_bytes<CurveBLS12377, false>()));
+  Arena arena(ctx);
+  DevBuf tmp;
+  int rc;
+  if ((rc = tmp.alloc(arena, gb))) return rc;
+  hipError_t e = hipMalloc(out, ib ? ib : 16);
+  if (e != hipSuccess) {
+    set_error(std::string("gm_points_upload hipMalloc: ") + hipGetErrorString(e));
+    return GM_ERR_OOM;
+  }
+  GM_HIP(hipMemcpyAsync(tmp.p, host_points, gb, hipMemcpyHostToDevice, ctx->stream));
+  if (curve == GM_BN254)
+    rc = g2 ? msm_prepare_points<CurveBN254, true>(ctx, tmp.p, n, *out)
+            : msm_prepare_points<CurveBN254, false>(ctx, tmp.p, n, *out);
+  else
+    rc = g2 ? msm_prepare_points<CurveBLS12377, true>(ctx, tmp.p, n, *out)
+            : msm_prepare_points<CurveBLS12377, false>(ctx, tmp.p, n, *out);
+  if (rc) return rc;
+  GM_HIP(hipStreamSynchronize(ctx->stream));
+  return GM_OK;
+}
+
+extern "C++" {
+template <class C, bool G2>
+static int msm_prepared_t(gm_ctx* ctx, const void* sc, const void* pts, size_t n, void* out_jac, void* out_aff) {
+  using HF = typename GroupSel<C, G2>::HF;
+  HF j[3];
+  int rc = msm_device<C, G2>(ctx, sc, pts, n, j, true);
+  if (rc) return rc;
+  if (out_jac) memcpy(out_jac, j, sizeof(j));
+  if (out_aff) {
+    host::Aff<HF> a = host::to_aff(host::Jac<HF>{j[0], j[1], j[2]});
+    memcpy(out_aff, &a, sizeof(a));
+  }
+  return GM_OK;
+}
+}  // extern "C++"
+
+int gm_msm_prepared(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const void* prepared, size_t n,
+                    void* out_jac, void* out_affine) {
+  if (!ctx) return GM_ERR_INVALID;
+  if (int rc = check_curve(curve)) return rc;
+  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  GM_HIP(hipSetDevice(ctx->device));
+  int rc;
+  if (curve == GM_BN254)
+    rc = g2 ? msm_prepared_t<CurveBN254, true>(ctx, scalars_dev, prepared, n, out_jac, out_affine)
+            : msm_prepared_t<CurveBN254, false>(ctx, scalars_dev, prepared, n, out_jac, out_affine);
+  else
+    rc = g2 ? msm_prepared_t<CurveBLS12377, true>(ctx, scalars_dev, prepared, n, out_jac, out_affine)
+            : msm_prepared_t<CurveBLS12377, false>(ctx, scalars_dev, prepared, n, out_jac, out_affine);
+  prof_collect(ctx);
+  return rc;
+}
+
+int gm_kzg_commit(gm_ctx* ctx, int curve, const void* srs, size_t srs_len, const void* coeffs_host, size_t n,
+                  void* digest_affine) {
+  if (!ctx || !digest_affine) return GM_ERR_INVALID;
+  if (n > srs_len) {
+    set_error("kzg commit: polynomial larger than the SRS");
+    return GM_ERR_INVALID;
+  }
+  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  GM_HIP(hipSetDevice(ctx->device));
+  Arena arena(ctx);
+  DevBuf s;
+  int rc;
+  if ((rc = s.alloc(arena, 32 * (n ? n : 1)))) return rc;
+  if (n) GM_HIP(hipMemcpyAsync(s.p, coeffs_host, 32 * n, hipMemcpyHostToDevice, ctx->stream));
+  return gm_msm_prepared(ctx, curve, 0, s.p, srs, n, nullptr, digest_affine);
+}
+
 // ---- NTT --------------------------------------------------------------------------
 int gm_ntt(gm_ctx* ctx, int curve, void* data_dev, size_t n, int inverse, int dit, int coset) {
   if (int rc = check_curve(curve)) return rc;

@@ -87,10 +87,10 @@ GM_DEV void xyzz_add_aff(XYZZ<F>& a, const Affine<F>& p) {
     a.zzz = FOps<F>::one();
     return;
   }
-  F U2 = fe_mul(p.x, a.zz);
-  F S2 = fe_mul(p.y, a.zzz);
-  F P = fe_sub(U2, a.x);
-  F R = fe_sub(S2, a.y);
+  // ordered so that each temporary dies as early as possible (register pressure
+  // decides the occupancy of the accumulation kernel, esp. for Fp2 coordinates)
+  F P = fe_sub(fe_mul(p.x, a.zz), a.x);   // U2 - X1
+  F R = fe_sub(fe_mul(p.y, a.zzz), a.y);  // S2 - Y1
   if (fe_is_zero(P)) {
     if (fe_is_zero(R)) {
       a = xyzz_dbl_aff(p);
@@ -101,13 +101,12 @@ GM_DEV void xyzz_add_aff(XYZZ<F>& a, const Affine<F>& p) {
   }
   F PP = fe_sqr(P);
   F PPP = fe_mul(P, PP);
-  F Q = fe_mul(a.x, PP);
-  F X3 = fe_sub(fe_sub(fe_sqr(R), PPP), fe_dbl(Q));
-  F Y3 = fe_sub(fe_mul(R, fe_sub(Q, X3)), fe_mul(a.y, PPP));
   a.zz = fe_mul(a.zz, PP);
+  F Q = fe_mul(a.x, PP);
   a.zzz = fe_mul(a.zzz, PPP);
+  F X3 = fe_sub(fe_sub(fe_sqr(R), PPP), fe_dbl(Q));
+  a.y = fe_sub(fe_mul(R, fe_sub(Q, X3)), fe_mul(a.y, PPP));
   a.x = X3;
-  a.y = Y3;
 }
 
 // 2*a (dbl-2008-s-1, a = 0).  Infinity maps to infinity (ZZ3 = V*0).

@@ -22,6 +22,9 @@
 #include "msm.hpp"
 #include "runtime.hpp"
 
+#include <cstdlib>
+#include <cstring>
+
 namespace gm {
 
 // ---------------------------------------------------------------------------
@@ -128,8 +131,8 @@ GM_DEV void accum_emit(uint32_t b, const XYZZ<F>& acc, bool is_first, bool is_la
   }
 }
 
-template <class F>
-__global__ void __launch_bounds__(128) k_msm_accum_seg(const uint32_t* __restrict__ points, uint32_t n,
+template <class F, bool PREFETCH>
+GM_DEV void accum_seg_body(const uint32_t* __restrict__ points, uint32_t n,
                                                        const uint32_t* __restrict__ keys,
                                                        const uint32_t* __restrict__ vals,
                                                        const uint32_t* __restrict__ offsets, uint32_t total,
@@ -158,7 +161,7 @@ __global__ void __launch_bounds__(128) k_msm_accum_seg(const uint32_t* __restric
     // prefetch the next point's words while this add runs
     uint32_t vn = 0;
     PackedPt<PW> Pn;
-    if (q + 1 < end) {
+    if (PREFETCH && q + 1 < end) {
       vn = vals[q + 1];
       const uint32_t in = vn & 0x7fffffffu;
       if (in >= n) {
@@ -173,13 +176,47 @@ __global__ void __launch_bounds__(128) k_msm_accum_seg(const uint32_t* __restric
       acc = xyzz_inf<F>();
       cur = k;
     }
+    if (!PREFETCH) P = load_packed_pt<PW>(points + (size_t)(v & 0x7fffffffu) * PW);
     Affine<F> A = load_affine_packed<F>(P.w);
     if (v >> 31) A.y = fe_neg(A.y);
     xyzz_add_aff(acc, A);
-    v = vn;
-    P = Pn;
+    if (PREFETCH) {
+      v = vn;
+      P = Pn;
+    } else if (q + 1 < end) {
+      v = vals[q + 1];
+      if ((v & 0x7fffffffu) >= n) {
+        atomicOr(err, 2u);
+        return;
+      }
+    }
   }
   accum_emit(cur, acc, first, true, start, end, t, offsets, buckets, part_first, part_last);
+}
+
+
+// G1: the next point is prefetched into registers while the current add runs.
+template <class F>
+__global__ void __launch_bounds__(128) k_msm_accum_seg(const uint32_t* __restrict__ points, uint32_t n,
+                                                       const uint32_t* __restrict__ keys,
+                                                       const uint32_t* __restrict__ vals,
+                                                       const uint32_t* __restrict__ offsets, uint32_t total,
+                                                       uint32_t K, XYZZ<F>* __restrict__ buckets,
+                                                       XYZZ<F>* __restrict__ part_first,
+                                                       XYZZ<F>* __restrict__ part_last, uint32_t* __restrict__ err) {
+  accum_seg_body<F, true>(points, n, keys, vals, offsets, total, K, buckets, part_first, part_last, err);
+}
+
+// G2 (Fp2 coordinates): a mixed add keeps ~330 registers live, i.e. one wave per
+// SIMD; without the prefetch and with the register budget capped at two waves
+// per SIMD the loads are hidden by the second wave instead.
+template <class F>
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2)))
+k_msm_accum_seg_g2(const uint32_t* __restrict__ points, uint32_t n, const uint32_t* __restrict__ keys,
+                   const uint32_t* __restrict__ vals, const uint32_t* __restrict__ offsets, uint32_t total,
+                   uint32_t K, XYZZ<F>* __restrict__ buckets, XYZZ<F>* __restrict__ part_first,
+                   XYZZ<F>* __restrict__ part_last, uint32_t* __restrict__ err) {
+  accum_seg_body<F, false>(points, n, keys, vals, offsets, total, K, buckets, part_first, part_last, err);
 }
 
 // Merge the partial sums of buckets cut by slice edges.  Bucket b spans slices
@@ -456,7 +493,13 @@ int msm_device(gm_ctx* ctx, const void* scalars_dev, const void* points_dev, siz
     if ((rc = plast.alloc(arena, sizeof(XYZZ<DF>) * nslices))) return rc;
     GM_HIP(hipMemsetAsync(buckets.p, 0, sizeof(XYZZ<DF>) * (size_t)total, st));  // all-zero XYZZ = infinity
     ProfScope ps(ctx, G2 ? "msm_accum_g2" : "msm_accum_g1");
-    hipLaunchKernelGGL(k_msm_accum_seg<DF>, dim3(blocks_for(nslices, 128)), dim3(128), 0, st, pts_internal,
+    // GM_MSM_ACCUM=prefetch|noprefetch overrides the per-group default (tuning)
+    static const char* ov = getenv("GM_MSM_ACCUM");
+    bool noprefetch = G2;
+    if (ov && !strcmp(ov, "prefetch")) noprefetch = false;
+    if (ov && !strcmp(ov, "noprefetch")) noprefetch = true;
+    auto accum = noprefetch ? k_msm_accum_seg_g2<DF> : k_msm_accum_seg<DF>;
+    hipLaunchKernelGGL(accum, dim3(blocks_for(nslices, 128)), dim3(128), 0, st, pts_internal,
                        (uint32_t)n, keys_out.as<uint32_t>(), sorted.as<uint32_t>(), offsets.as<uint32_t>(), total,
                        K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>(),
                        errw.as<uint32_t>());

@@ -40,7 +40,7 @@ SYMBOLS = [
     "gm_last_error", "gm_version", "gm_init", "gm_destroy", "gm_synchronize",
     "gm_profile_enable", "gm_profile_reset", "gm_profile_get", "gm_profile_dump",
     "gm_set_msm_window", "gm_malloc", "gm_free", "gm_copy_to_device", "gm_memcpy_h2d",
-    "gm_memcpy_d2h", "gm_memcpy_d2d", "gm_copy_points_to_device", "gm_msm", "gm_msm_host_scalars", "gm_ntt",
+    "gm_memcpy_d2h", "gm_memcpy_d2d", "gm_copy_points_to_device", "gm_msm", "gm_msm_host_scalars", "gm_points_upload", "gm_msm_prepared", "gm_kzg_commit", "gm_ntt",
     "gm_poly_ops", "gm_reverse_scalars", "gm_groth16_compute_h", "gm_g16_pk_upload",
     "gm_g16_pk_free", "gm_g16_prove", "gm_g16_prove_device", "gm_jac_add", "gm_jac_to_affine",
     "gm_batch_mul_base", "gm_random_scalars", "gm_generator", "gm_test_field_op",
@@ -83,6 +83,9 @@ def load_library(path: str = LIB_PATH):
     L.gm_copy_points_to_device.argtypes = [vp, i, i, vp, sz, pvp]
     L.gm_msm.argtypes = [vp, i, i, vp, vp, sz, vp, vp]
     L.gm_msm_host_scalars.argtypes = [vp, i, i, vp, vp, sz, vp, vp]
+    L.gm_points_upload.argtypes = [vp, i, i, vp, sz, pvp]
+    L.gm_msm_prepared.argtypes = [vp, i, i, vp, vp, sz, vp, vp]
+    L.gm_kzg_commit.argtypes = [vp, i, vp, sz, vp, sz, vp]
     L.gm_ntt.argtypes = [vp, i, vp, sz, i, i, i]
     L.gm_poly_ops.argtypes = [vp, i, vp, vp, vp, sz, vp]
     L.gm_reverse_scalars.argtypes = [vp, i, vp, sz]
@@ -250,6 +253,31 @@ class Context:
         pp = points.ptr if isinstance(points, DeviceBuffer) else points
         _check(load_library().gm_msm(self.handle, curve_id(curve), int(g2), sp, pp, n, _p(jac), _p(aff)))
         return jac.tobytes(), aff.tobytes()
+
+    def points_upload(self, curve, points, g2: bool = False) -> DeviceBuffer:
+        """Device-resident point set in the MSM's internal layout (pk arrays, SRS)."""
+        a = _buf(points)
+        n = a.size // point_bytes(curve, g2)
+        p = ctypes.c_void_p()
+        _check(load_library().gm_points_upload(self.handle, curve_id(curve), int(g2), _p(a), n, ctypes.byref(p)))
+        buf = DeviceBuffer(self, p.value, a.size)
+        buf.count = n
+        return buf
+
+    def msm_prepared(self, curve, scalars: DeviceBuffer, prepared: DeviceBuffer, n: int, g2: bool = False):
+        jac = np.zeros(jac_bytes(curve, g2), np.uint8)
+        aff = np.zeros(point_bytes(curve, g2), np.uint8)
+        _check(load_library().gm_msm_prepared(self.handle, curve_id(curve), int(g2), scalars.ptr, prepared.ptr, n,
+                                              _p(jac), _p(aff)))
+        return jac.tobytes(), aff.tobytes()
+
+    def kzg_commit(self, curve, srs: DeviceBuffer, coeffs) -> bytes:
+        """kzg.Commit(p, pk): G1 digest of the polynomial coefficients (host)."""
+        c = _buf(coeffs)
+        out = np.zeros(point_bytes(curve, False), np.uint8)
+        _check(load_library().gm_kzg_commit(self.handle, curve_id(curve), srs.ptr, srs.count, _p(c),
+                                            c.size // FR_BYTES, _p(out)))
+        return out.tobytes()
 
     def msm_on_device(self, scalars, points, n, curve="bn254"):
         """MsmOnDevice(scalars_d, points_d, count, convert=true) -> G1Jac bytes."""

@@ -84,6 +84,23 @@ int gm_msm(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const void* 
 int gm_msm_host_scalars(gm_ctx* ctx, int curve, int g2, const void* scalars_host,
                         const void* points_dev, size_t n, void* out_jac, void* out_affine);
 
+/* Device-resident point sets (a proving key's arrays, a KZG SRS): upload n gnark
+ * affine points once, converted to the MSM's internal layout (same byte size),
+ * and run MSMs over any prefix of them without per-call conversion.  Free with
+ * gm_free.  (setupDevicePointers, icicle.go:90-125, keeps pk points resident.) */
+int gm_points_upload(gm_ctx* ctx, int curve, int g2, const void* host_points, size_t n,
+                     void** prepared_out);
+int gm_msm_prepared(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const void* prepared,
+                    size_t n, void* out_jac, void* out_affine);
+
+/* ---- KZG commitment (PLONK; backend/plonk/bls12-377/prove.go:312,460,718,
+ *      1158-1168 call gnark-crypto kzg.Commit) ---------------------------------
+ * digest = sum_i coeffs[i] * srs[i] over the first n points of a prepared SRS
+ * (pk.Kzg.G1 or pk.KzgLagrange.G1, setup.go:81-82), coeffs = n Montgomery
+ * fr.Elements in host memory.  GM_ERR_INVALID if n > srs_len (kzg.ErrInvalidPolynomialSize). */
+int gm_kzg_commit(gm_ctx* ctx, int curve, const void* srs_prepared, size_t srs_len,
+                  const void* coeffs_host, size_t n, void* digest_affine);
+
 /* ---- NTT (iciclegnark GenerateTwiddleFactors icicle.go:68,73;
  *      INttOnDevice :489,502; NttOnDevice :490; PolyOps :500;
  *      ReverseScalars :510; CPU twin fft.Domain.FFT/FFTInverse

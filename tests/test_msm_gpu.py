@@ -129,3 +129,54 @@ def test_msm_skewed_scalars(gm_ctx, oracle):
     assert aff == oracle.msm("bn254", False, sb, P.to_host())
     for b in (S, K, P):
         b.free()
+
+
+@pytest.mark.parametrize("cname,g2,logn", [("bn254", False, 20), ("bn254", True, 18), ("bls12377", False, 20)])
+def test_msm_huge_buckets_large(gm_ctx, oracle, cname, g2, logn):
+    """Buckets spanning thousands of accumulation slices (tree-reduced fixup):
+    wire-like scalars in {0, 1, 2, r-1} plus 1% random; the bls12377 case also
+    has the nearly empty top window of a 253-bit field."""
+    import gnark_mi355x as gm
+    c = pyref.CURVES[cname]
+    n = 1 << logn
+    rng = np.random.default_rng(logn)
+    table = np.frombuffer(b"".join(pyref.encode_fr(c, v) for v in (0, 1, 2, c.r - 1)), np.uint8).reshape(4, 32)
+    sb = table[rng.integers(0, 4, n)].copy()
+    R = gm_ctx.random_scalars(cname, n // 100, seed=logn)
+    sb[:: 100][: n // 100] = np.frombuffer(R.to_host(), np.uint8).reshape(-1, 32)[: len(sb[::100])]
+    R.free()
+    sb = sb.tobytes()
+    K = gm_ctx.random_scalars(cname, n, seed=5)
+    P = gm_ctx.batch_mul_base(cname, g2, gm.generator(cname, g2), K, n)
+    S = gm_ctx.copy_to_device(sb)
+    _, aff = gm_ctx.msm(cname, S, P, n, g2=g2)
+    assert aff == oracle.msm(cname, g2, sb, P.to_host())
+    for b in (S, K, P):
+        b.free()
+
+
+@pytest.mark.parametrize("cname", ["bls12377", "bn254"])
+def test_kzg_commit_and_prepared_msm(gm_ctx, oracle, cname):
+    """PLONK KZG commit (kzg.Commit over pk.Kzg.G1, backend/plonk/bls12-377/prove.go:
+    1158-1168): digest of a polynomial over a prefix of a device-resident SRS."""
+    import gnark_mi355x as gm
+    c = pyref.CURVES[cname]
+    m = 5000
+    tau = pyref.random_scalars(c, 1, 11)[0]
+    powers = b"".join(pyref.encode_fr(c, pow(tau, i, c.r)) for i in range(m))
+    srs_host = oracle.batch_mul_base(cname, False, gm.generator(cname), powers)
+    srs = gm_ctx.points_upload(cname, srs_host)
+    for n in (0, 1, 17, 4096, m):
+        coeffs = b"".join(pyref.encode_fr(c, v) for v in pyref.random_scalars(c, n, n + 3))
+        got = gm_ctx.kzg_commit(cname, srs, coeffs)
+        pb = gm.point_bytes(cname, False)
+        exp = oracle.msm(cname, False, coeffs, srs_host[:pb * n]) if n else bytes(pb)
+        assert got == exp, n
+    with pytest.raises(gm.GmError):
+        gm_ctx.kzg_commit(cname, srs, bytes(32 * (m + 1)))
+    # generic prepared MSM equals the raw-buffer MSM
+    S = gm_ctx.random_scalars(cname, m, seed=9)
+    P = gm_ctx.copy_to_device(srs_host)
+    assert gm_ctx.msm_prepared(cname, S, srs, m)[1] == gm_ctx.msm(cname, S, P, m)[1]
+    for b in (S, P, srs):
+        b.free()
