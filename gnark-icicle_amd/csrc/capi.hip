@@ -4,6 +4,7 @@
 // CPU prover groth16_bn254.Prove (backend/groth16/bn254/prove.go:62-325) as
 // SURVEY.md §0.3 prescribes: only the MSMs and NTTs move to the device.
 #include <cstring>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -652,8 +653,7 @@ static int g16_prove_t(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, void* 
   hipStream_t st = ctx->stream;
   const size_t n = pk->n;
   int rc;
-  // H (computeH, icicle.go:453-513 / prove.go:356-399) -> bit-reversed h in `a`
-  if ((rc = compute_h_device<C>(ctx, a, b, c, nc, n))) return rc;
+
   // device-side scalar compaction (icicle.go:231-278 do this on the host + H2D)
   Arena arena(ctx);
   DevBuf wA, wB, wK;
@@ -680,29 +680,57 @@ static int g16_prove_t(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, void* 
   memcpy(&alpha, pk->alpha.data(), sizeof(alpha));
   memcpy(&beta, pk->beta.data(), sizeof(beta));
   memcpy(&delta, pk->delta.data(), sizeof(delta));
+  // [r]delta, [s]delta, [kr]delta (BatchScalarMultiplicationG1, prove.go:195) and
+  // [s]delta2 do not depend on the device results: computed on a host thread
+  // while the GPU runs computeH and the MSMs.
   J1 dj = host::to_jac(delta);
-  J1 d0 = host::jmul(dj, rc_.v, 4), d1 = host::jmul(dj, sc_.v, 4), d2 = host::jmul(dj, krc.v, 4);
+  host::Aff<HF2> beta2, delta2;
+  memcpy(&beta2, pk->beta2.data(), sizeof(beta2));
+  memcpy(&delta2, pk->delta2.data(), sizeof(delta2));
+  J1 d0, d1, d2;
+  J2 sd2;
+  std::thread deltas([&] {
+    d0 = host::jmul(dj, rc_.v, 4);
+    d1 = host::jmul(dj, sc_.v, 4);
+    d2 = host::jmul(dj, krc.v, 4);
+    sd2 = host::jmul(host::to_jac(delta2), sc_.v, 4);
+  });
+  struct Joiner {
+    std::thread& t;
+    ~Joiner() {
+      if (t.joinable()) t.join();
+    }
+  } joiner{deltas};
+  // H (computeH, icicle.go:453-513 / prove.go:356-399) -> bit-reversed h in `a`
+  if ((rc = compute_h_device<C>(ctx, a, b, c, nc, n))) return rc;
   HF1 t1[3];
-  // Ar = MSM(wA, A) + alpha + r delta   (computeAR1 icicle.go:312-324)
+  // MSM results are combined below only after the delta thread has finished
   if ((rc = msm_device<C, false>(ctx, wA.p, pk->A, pk->nbA, t1, true))) return rc;
+  deltas.join();
+  // Ar = MSM(wA, A) + alpha + r delta   (computeAR1 icicle.go:312-324)
   J1 ar = host::jadd(host::jadd_aff(J1{t1[0], t1[1], t1[2]}, alpha), d0);
   // Bs1 = MSM(wB, B) + beta + s delta   (computeBS1 icicle.go:299-310)
   if ((rc = msm_device<C, false>(ctx, wB.p, pk->B, pk->nbB, t1, true))) return rc;
   J1 bs1 = host::jadd(host::jadd_aff(J1{t1[0], t1[1], t1[2]}, beta), d1);
+  // [s]Ar and [r]Bs1 on a host thread while the GPU runs the K, Z and G2 MSMs
+  J1 s_ar, r_bs1;
+  std::thread cross([&] {
+    s_ar = host::jmul(ar, sc_.v, 4);
+    r_bs1 = host::jmul(bs1, rc_.v, 4);
+  });
+  Joiner joiner2{cross};
   // Krs = MSM(wK, K) + kr delta + MSM(h[:n-1], Z) + s Ar + r Bs1   (computeKRS icicle.go:326-375)
   if ((rc = msm_device<C, false>(ctx, wK.p, pk->K, pk->nbK, t1, true))) return rc;
   J1 krs = host::jadd(J1{t1[0], t1[1], t1[2]}, d2);
   if ((rc = msm_device<C, false>(ctx, a, pk->Z, n - 1, t1, true))) return rc;
   krs = host::jadd(krs, J1{t1[0], t1[1], t1[2]});
-  krs = host::jadd(krs, host::jmul(ar, sc_.v, 4));
-  krs = host::jadd(krs, host::jmul(bs1, rc_.v, 4));
   // Bs = MSM_G2(wB, B2) + s delta2 + beta2   (computeBS2 icicle.go:377-393)
   HF2 t2[3];
   if ((rc = msm_device<C, true>(ctx, wB.p, pk->B2, pk->nbB, t2, true))) return rc;
-  host::Aff<HF2> beta2, delta2;
-  memcpy(&beta2, pk->beta2.data(), sizeof(beta2));
-  memcpy(&delta2, pk->delta2.data(), sizeof(delta2));
-  J2 bs = host::jadd(J2{t2[0], t2[1], t2[2]}, host::jmul(host::to_jac(delta2), sc_.v, 4));
+  cross.join();
+  krs = host::jadd(krs, s_ar);
+  krs = host::jadd(krs, r_bs1);
+  J2 bs = host::jadd(J2{t2[0], t2[1], t2[2]}, sd2);
   bs = host::jadd_aff(bs, beta2);
   host::Aff<HF1> ara = host::to_aff(ar), krsa = host::to_aff(krs);
   host::Aff<HF2> bsa = host::to_aff(bs);

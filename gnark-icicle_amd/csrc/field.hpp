@@ -407,14 +407,20 @@ GM_DEV Fe2<P, BETA> fe_mul(const Fe2<P, BETA>& a, const Fe2<P, BETA>& b) {
   r.a1 = fe_sub(fe_sub(s, v0), v1);
   return r;
 }
+// Complex squaring, 2 base multiplications:
+//   a0^2 + BETA a1^2 = (a0 + a1)(a0 + BETA a1) - (1 + BETA) a0 a1,  2 a0 a1 u
 template <class P, int BETA>
 GM_DEV Fe2<P, BETA> fe_sqr(const Fe2<P, BETA>& a) {
-  // (a0 + a1 u)^2 = a0^2 + BETA a1^2 + 2 a0 a1 u
-  Fe<P> v0 = fe_sqr(a.a0);
-  Fe<P> v1 = fe_sqr(a.a1);
-  Fe<P> c = fe_mul(a.a0, a.a1);
+  const Fe<P> c = fe_mul(a.a0, a.a1);
+  Fe<P> t = fe_mul(fe_add(a.a0, a.a1), fe_add(a.a0, mul_by_beta<P, BETA>(a.a1)));
+  if constexpr (BETA == -5) {
+    const Fe<P> c2 = fe_dbl(c);
+    t = fe_add(t, fe_dbl(c2));  // - (1 + BETA) c = + 4c
+  } else {
+    static_assert(BETA == -1, "unsupported non-residue");
+  }
   Fe2<P, BETA> r;
-  r.a0 = fe_add(v0, mul_by_beta<P, BETA>(v1));
+  r.a0 = t;
   r.a1 = fe_dbl(c);
   return r;
 }
