@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--ntt-logn", type=int, default=24)
     ap.add_argument("--g16-logn", type=str, default="20,24", help="Groth16 prove domains, comma list ('' = skip)")
     ap.add_argument("--msm-extra", type=int, default=1, help="secondary G2 / BLS12-377 MSM lines (0 = skip)")
+    ap.add_argument("--g16-plain", type=str, default="20",
+                    help="Groth16 domains also proved with a plain (non-precomputed) pk")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
     return ap.parse_args()
@@ -197,30 +199,46 @@ def secondary(ctx, gm, args):
         res["msm"] = {}
         for curve, g2, logn in (("bn254", True, 20), ("bls12377", False, 22), ("bls12377", True, 22)):
             res["msm"]["%s_%s_2^%d" % (curve, "g2" if g2 else "g1", logn)] = msm_line(ctx, gm, curve, g2, logn)
+        for curve, g2, logn in (("bn254", False, 20), ("bn254", True, 20)):
+            res["msm"]["%s_%s_2^%d_precomputed" % (curve, "g2" if g2 else "g1", logn)] = \
+                msm_line(ctx, gm, curve, g2, logn, precompute=True)
     if args.g16_logn:
-        res["groth16"] = [groth16_bench(ctx, gm, int(l)) for l in args.g16_logn.split(",") if l]
+        plain = [int(l) for l in args.g16_plain.split(",") if l]
+        res["groth16"] = []
+        for l in (int(x) for x in args.g16_logn.split(",") if x):
+            if l in plain:
+                res["groth16"].append(groth16_bench(ctx, gm, l, precompute=False))
+            res["groth16"].append(groth16_bench(ctx, gm, l, precompute=True))
     return res
 
 
-def msm_line(ctx, gm, curve, g2, logn, reps=5):
-    """Mpoints/s of one more MSM configuration (BASELINE configs[4]: BLS12-377 G1+G2 2^22)."""
+def msm_line(ctx, gm, curve, g2, logn, reps=5, precompute=False):
+    """Mpoints/s of one more MSM configuration (BASELINE configs[4]: BLS12-377 G1+G2 2^22).
+    precompute: fixed-base window copies prepared once, untimed (a pk / SRS)."""
     n = 1 << logn
     S = ctx.random_scalars(curve, n, 0x5EED0005)
     K = ctx.random_scalars(curve, n, 0x5EED1005)
     P = ctx.batch_mul_base(curve, g2, gm.generator(curve, g2), K, n)
     K.free()
-    ctx.msm(curve, S, P, n, g2=g2)
+    if precompute:
+        pre = ctx.points_upload_precomputed(curve, P.to_host(), g2, 0)
+        P.free()
+        P = pre
+        run = lambda: ctx.msm_precomputed(curve, S, pre, n, g2=g2)
+    else:
+        run = lambda: ctx.msm(curve, S, P, n, g2=g2)
+    run()
     ctx.synchronize()
     t0 = time.perf_counter()
     for _ in range(reps):
-        ctx.msm(curve, S, P, n, g2=g2)
+        run()
     dt = (time.perf_counter() - t0) / reps
     S.free()
     P.free()
     return {"mpoints_per_s": round(n / dt / 1e6, 3), "ms": round(dt * 1e3, 3)}
 
 
-def groth16_bench(ctx, gm, logn):
+def groth16_bench(ctx, gm, logn, precompute=True):
     """Groth16 prove at n = 2^logn with a synthetic proving key (random points,
     the DummySetup-style timing setup of groth16_test.go:70-88) and synthetic
     solution vectors; timer scope = icicle.go:204-412 (after Solve)."""
@@ -244,7 +262,8 @@ def groth16_bench(ctx, gm, logn):
           "g1_A": pts(nb_wires, False, 3), "g1_B": pts(nb_wires, False, 4), "g1_Z": pts(n - 1, False, 5),
           "g1_K": pts(nb_wires - nb_public, False, 6), "g2_beta": one2[:128], "g2_delta": one2[128:256],
           "g2_B": pts(nb_wires, True, 7), "infA": np.zeros(nb_wires, np.uint8), "infB": np.zeros(nb_wires, np.uint8)}
-    dpk = gm.ProvingKey(ctx, "bn254", pk, n, nb_wires, nb_public)
+    dpk = gm.ProvingKey(ctx, "bn254", pk, n, nb_wires, nb_public, precompute=precompute)
+    del pk
     W = ctx.random_scalars("bn254", nb_wires, 8)
     A, B, C = (ctx.malloc(32 * n) for _ in range(3))
     srcs = [ctx.random_scalars("bn254", n, 9 + i) for i in range(3)]
@@ -260,7 +279,8 @@ def groth16_bench(ctx, gm, logn):
     dpk.free()
     for b in [W, A, B, C] + srcs:
         b.free()
-    return {"logn": logn, "prove_ms": round(min(times) * 1e3, 3), "note": "inputs device-resident; after Solve"}
+    return {"logn": logn, "prove_ms": round(min(times) * 1e3, 3), "pk": "precomputed" if precompute else "plain",
+            "note": "inputs device-resident; after Solve"}
 
 
 def cpu_baseline(S, P, n, gpu_jac):

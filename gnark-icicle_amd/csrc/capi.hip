@@ -132,6 +132,8 @@ struct gm_g16_pk {
   size_t n, nb_wires, nb_public, nbA, nbB, nbK;
   void *A, *B, *Z, *K, *B2;       // device point arrays
   void *idxA, *idxB, *idxK;       // device index maps (compaction)
+  bool precomp = false;           // GM_PK_PRECOMPUTE: fixed-base window copies
+  MsmPrecomp preA, preB, preZ, preK;  // layouts (B and B2 share preB)
   std::vector<uint8_t> alpha, beta, delta, beta2, delta2;  // host affine
 };
 
@@ -345,10 +347,11 @@ int gm_points_upload(gm_ctx* ctx, int curve, int g2, const void* host_points, si
 
 extern "C++" {
 template <class C, bool G2>
-static int msm_prepared_t(gm_ctx* ctx, const void* sc, const void* pts, size_t n, void* out_jac, void* out_aff) {
+static int msm_prepared_t(gm_ctx* ctx, const void* sc, const void* pts, size_t n, void* out_jac, void* out_aff,
+                          const MsmPrecomp* pre = nullptr) {
   using HF = typename GroupSel<C, G2>::HF;
   HF j[3];
-  int rc = msm_device<C, G2>(ctx, sc, pts, n, j, true);
+  int rc = msm_device<C, G2>(ctx, sc, pts, n, j, true, pre);
   if (rc) return rc;
   if (out_jac) memcpy(out_jac, j, sizeof(j));
   if (out_aff) {
@@ -372,6 +375,94 @@ int gm_msm_prepared(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, con
   else
     rc = g2 ? msm_prepared_t<CurveBLS12377, true>(ctx, scalars_dev, prepared, n, out_jac, out_affine)
             : msm_prepared_t<CurveBLS12377, false>(ctx, scalars_dev, prepared, n, out_jac, out_affine);
+  prof_collect(ctx);
+  return rc;
+}
+
+// ---- fixed-base precomputed point sets -------------------------------------------
+static int make_precomp(int curve, size_t n, int window, MsmPrecomp* out) {
+  const int bits = curve == GM_BN254 ? CurveBN254::FR_BITS : CurveBLS12377::FR_BITS;
+  if (window == 0) {
+    *out = msm_choose_precomp(n, bits);
+    return GM_OK;
+  }
+  if (window < 2 || window > 24) {
+    set_error("precompute: window must be 0 (auto) or in [2, 24]");
+    return GM_ERR_INVALID;
+  }
+  out->c = (uint32_t)window;
+  out->W = (uint32_t)((bits + 1 + window - 1) / window);
+  out->stride = n;
+  return GM_OK;
+}
+
+int gm_precompute_layout(int curve, size_t n, int window, int* c_out, int* copies_out) {
+  if (int rc = check_curve(curve)) return rc;
+  MsmPrecomp p;
+  if (int rc = make_precomp(curve, n, window, &p)) return rc;
+  if (c_out) *c_out = (int)p.c;
+  if (copies_out) *copies_out = (int)p.W;
+  return GM_OK;
+}
+
+int gm_points_upload_precomputed(gm_ctx* ctx, int curve, int g2, const void* host_points, size_t n, int window,
+                                 void** out) {
+  if (!ctx || !out) return GM_ERR_INVALID;
+  if (int rc = check_curve(curve)) return rc;
+  MsmPrecomp pre;
+  if (int rc = make_precomp(curve, n, window, &pre)) return rc;
+  if ((size_t)pre.W * n >= (size_t(1) << 31)) {
+    set_error("precompute: copies * n must be < 2^31");
+    return GM_ERR_INVALID;
+  }
+  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  GM_HIP(hipSetDevice(ctx->device));
+  const size_t gb = fp_bytes(curve) * (g2 ? 4 : 2) * n;
+  const size_t ib = (size_t)pre.W * n *
+                    (curve == GM_BN254 ? (g2 ? msm_internal_point_bytes<CurveBN254, true>()
+                                             : msm_internal_point_bytes<CurveBN254, false>())
+                                       : (g2 ? msm_internal_point_bytes<CurveBLS12377, true>()
+                                             : msm_internal_point_bytes<CurveBLS12377, false>()));
+  Arena arena(ctx);
+  DevBuf tmp;
+  int rc;
+  if ((rc = tmp.alloc(arena, gb ? gb : 16))) return rc;
+  hipError_t e = hipMalloc(out, ib ? ib : 16);
+  if (e != hipSuccess) {
+    set_error(std::string("gm_points_upload_precomputed hipMalloc: ") + hipGetErrorString(e));
+    return GM_ERR_OOM;
+  }
+  if (gb) GM_HIP(hipMemcpyAsync(tmp.p, host_points, gb, hipMemcpyHostToDevice, ctx->stream));
+  if (curve == GM_BN254)
+    rc = g2 ? msm_precompute_points<CurveBN254, true>(ctx, tmp.p, n, pre, *out)
+            : msm_precompute_points<CurveBN254, false>(ctx, tmp.p, n, pre, *out);
+  else
+    rc = g2 ? msm_precompute_points<CurveBLS12377, true>(ctx, tmp.p, n, pre, *out)
+            : msm_precompute_points<CurveBLS12377, false>(ctx, tmp.p, n, pre, *out);
+  if (rc) return rc;
+  GM_HIP(hipStreamSynchronize(ctx->stream));
+  return GM_OK;
+}
+
+int gm_msm_precomputed(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const void* prepared,
+                       size_t prepared_n, int window, size_t n, void* out_jac, void* out_affine) {
+  if (!ctx) return GM_ERR_INVALID;
+  if (int rc = check_curve(curve)) return rc;
+  if (n > prepared_n) {
+    set_error("msm_precomputed: n exceeds the prepared point count");
+    return GM_ERR_INVALID;
+  }
+  MsmPrecomp pre;
+  if (int rc = make_precomp(curve, prepared_n, window, &pre)) return rc;
+  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  GM_HIP(hipSetDevice(ctx->device));
+  int rc;
+  if (curve == GM_BN254)
+    rc = g2 ? msm_prepared_t<CurveBN254, true>(ctx, scalars_dev, prepared, n, out_jac, out_affine, &pre)
+            : msm_prepared_t<CurveBN254, false>(ctx, scalars_dev, prepared, n, out_jac, out_affine, &pre);
+  else
+    rc = g2 ? msm_prepared_t<CurveBLS12377, true>(ctx, scalars_dev, prepared, n, out_jac, out_affine, &pre)
+            : msm_prepared_t<CurveBLS12377, false>(ctx, scalars_dev, prepared, n, out_jac, out_affine, &pre);
   prof_collect(ctx);
   return rc;
 }
@@ -532,7 +623,15 @@ int gm_batch_mul_base(gm_ctx* ctx, int curve, int g2, const void* base, const vo
 
 // ---- Groth16 ------------------------------------------------------------------------------
 int gm_g16_pk_upload(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, gm_g16_pk** out) {
+  return gm_g16_pk_upload_ex(ctx, curve, h, 0u, out);
+}
+
+int gm_g16_pk_upload_ex(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsigned flags, gm_g16_pk** out) {
   if (int rc = check_curve(curve)) return rc;
+  if (flags & ~(unsigned)GM_PK_PRECOMPUTE) {
+    set_error("pk upload: unknown flags");
+    return GM_ERR_INVALID;
+  }
   if (!h || !out || h->domain_size < 2) return GM_ERR_INVALID;
   std::lock_guard<std::recursive_mutex> g(ctx->mu);
   GM_HIP(hipSetDevice(ctx->device));
@@ -544,6 +643,14 @@ int gm_g16_pk_upload(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, gm_g16_pk*
   pk->nbA = h->nbA;
   pk->nbB = h->nbB;
   pk->nbK = h->nbK;
+  pk->precomp = (flags & GM_PK_PRECOMPUTE) != 0;
+  const int frbits = curve == GM_BN254 ? CurveBN254::FR_BITS : CurveBLS12377::FR_BITS;
+  if (pk->precomp) {
+    pk->preA = msm_choose_precomp(pk->nbA, frbits);
+    pk->preB = msm_choose_precomp(pk->nbB, frbits);
+    pk->preZ = msm_choose_precomp(pk->n - 1, frbits);
+    pk->preK = msm_choose_precomp(pk->nbK, frbits);
+  }
   const size_t g1b = 2 * fp_bytes(curve), g2b = 4 * fp_bytes(curve);
   auto up = [&](const void* src, size_t bytes, void** dst) -> int {
     hipError_t e = hipMalloc(dst, bytes ? bytes : 16);
@@ -563,32 +670,44 @@ int gm_g16_pk_upload(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, gm_g16_pk*
   int rc;
   // upload gnark-layout points, convert once into the device-internal layout
   // (radix-2^29 Montgomery) the MSM kernels consume (setupDevicePointers).
-  auto up_pts = [&](const void* src, size_t count, bool g2, void** dst) -> int {
+  // (with GM_PK_PRECOMPUTE also the W-1 window-shifted copies, msm_precompute_points)
+  auto up_pts = [&](const void* src, size_t count, bool g2, const MsmPrecomp& pre, void** dst) -> int {
     void* tmp = nullptr;
     int r = up(src, (g2 ? g2b : g1b) * count, &tmp);
     if (r) return r;
     size_t ib = 0;
     if (curve == GM_BN254) ib = g2 ? msm_internal_point_bytes<CurveBN254, true>() : msm_internal_point_bytes<CurveBN254, false>();
     else ib = g2 ? msm_internal_point_bytes<CurveBLS12377, true>() : msm_internal_point_bytes<CurveBLS12377, false>();
-    hipError_t e = hipMalloc(dst, ib * (count ? count : 1));
+    const size_t copies = pk->precomp ? pre.W : 1;
+    hipError_t e = hipMalloc(dst, ib * (count ? count * copies : 1));
     if (e != hipSuccess) {
       hipFree(tmp);
       set_error(std::string("pk upload hipMalloc: ") + hipGetErrorString(e));
       return GM_ERR_OOM;
     }
-    if (curve == GM_BN254)
+    if (pk->precomp) {
+      if (curve == GM_BN254)
+        r = g2 ? msm_precompute_points<CurveBN254, true>(ctx, tmp, count, pre, *dst)
+               : msm_precompute_points<CurveBN254, false>(ctx, tmp, count, pre, *dst);
+      else
+        r = g2 ? msm_precompute_points<CurveBLS12377, true>(ctx, tmp, count, pre, *dst)
+               : msm_precompute_points<CurveBLS12377, false>(ctx, tmp, count, pre, *dst);
+    } else if (curve == GM_BN254) {
       r = g2 ? msm_prepare_points<CurveBN254, true>(ctx, tmp, count, *dst)
              : msm_prepare_points<CurveBN254, false>(ctx, tmp, count, *dst);
-    else
+    } else {
       r = g2 ? msm_prepare_points<CurveBLS12377, true>(ctx, tmp, count, *dst)
              : msm_prepare_points<CurveBLS12377, false>(ctx, tmp, count, *dst);
+    }
     hipStreamSynchronize(ctx->stream);
     hipFree(tmp);
     return r;
   };
-  if ((rc = up_pts(h->g1_A, pk->nbA, false, &pk->A)) || (rc = up_pts(h->g1_B, pk->nbB, false, &pk->B)) ||
-      (rc = up_pts(h->g1_Z, pk->n - 1, false, &pk->Z)) || (rc = up_pts(h->g1_K, pk->nbK, false, &pk->K)) ||
-      (rc = up_pts(h->g2_B, pk->nbB, true, &pk->B2))) {
+  if ((rc = up_pts(h->g1_A, pk->nbA, false, pk->preA, &pk->A)) ||
+      (rc = up_pts(h->g1_B, pk->nbB, false, pk->preB, &pk->B)) ||
+      (rc = up_pts(h->g1_Z, pk->n - 1, false, pk->preZ, &pk->Z)) ||
+      (rc = up_pts(h->g1_K, pk->nbK, false, pk->preK, &pk->K)) ||
+      (rc = up_pts(h->g2_B, pk->nbB, true, pk->preB, &pk->B2))) {
     delete pk;
     return rc;
   }
@@ -704,15 +823,30 @@ static int g16_prove_t(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, void* 
   // H (computeH, icicle.go:453-513 / prove.go:356-399) -> bit-reversed h in `a`
   if ((rc = compute_h_device<C>(ctx, a, b, c, nc, n))) return rc;
   HF1 t1[3];
+  const MsmPrecomp* pA = pk->precomp ? &pk->preA : nullptr;
+  const MsmPrecomp* pB = pk->precomp ? &pk->preB : nullptr;
+  const MsmPrecomp* pK = pk->precomp ? &pk->preK : nullptr;
+  const MsmPrecomp* pZ = pk->precomp ? &pk->preZ : nullptr;
   // MSM results are combined below only after the delta thread has finished
-  if ((rc = msm_device<C, false>(ctx, wA.p, pk->A, pk->nbA, t1, true))) return rc;
+  if ((rc = msm_device<C, false>(ctx, wA.p, pk->A, pk->nbA, t1, true, pA))) return rc;
   deltas.join();
   // Ar = MSM(wA, A) + alpha + r delta   (computeAR1 icicle.go:312-324)
   J1 ar = host::jadd(host::jadd_aff(J1{t1[0], t1[1], t1[2]}, alpha), d0);
-  // Bs1 = MSM(wB, B) + beta + s delta   (computeBS1 icicle.go:299-310)
-  if ((rc = msm_device<C, false>(ctx, wB.p, pk->B, pk->nbB, t1, true))) return rc;
-  J1 bs1 = host::jadd(host::jadd_aff(J1{t1[0], t1[1], t1[2]}, beta), d1);
-  // [s]Ar and [r]Bs1 on a host thread while the GPU runs the K, Z and G2 MSMs
+  // The G1 and G2 B-MSMs (prove.go:217,293) share scalars and layout: one
+  // sorted digit plan serves both.
+  HF2 t2[3];
+  J1 bs1;
+  {
+    Arena parena(ctx);
+    MsmPlan planB;
+    if ((rc = msm_plan<C>(ctx, parena, wB.p, pk->nbB, pB, planB))) return rc;
+    // Bs1 = MSM(wB, B) + beta + s delta   (computeBS1 icicle.go:299-310)
+    if ((rc = msm_run<C, false>(ctx, planB, pk->B, t1))) return rc;
+    bs1 = host::jadd(host::jadd_aff(J1{t1[0], t1[1], t1[2]}, beta), d1);
+    // Bs = MSM_G2(wB, B2) + s delta2 + beta2   (computeBS2 icicle.go:377-393)
+    if ((rc = msm_run<C, true>(ctx, planB, pk->B2, t2))) return rc;
+  }
+  // [s]Ar and [r]Bs1 on a host thread while the GPU runs the K and Z MSMs
   J1 s_ar, r_bs1;
   std::thread cross([&] {
     s_ar = host::jmul(ar, sc_.v, 4);
@@ -720,13 +854,10 @@ static int g16_prove_t(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, void* 
   });
   Joiner joiner2{cross};
   // Krs = MSM(wK, K) + kr delta + MSM(h[:n-1], Z) + s Ar + r Bs1   (computeKRS icicle.go:326-375)
-  if ((rc = msm_device<C, false>(ctx, wK.p, pk->K, pk->nbK, t1, true))) return rc;
+  if ((rc = msm_device<C, false>(ctx, wK.p, pk->K, pk->nbK, t1, true, pK))) return rc;
   J1 krs = host::jadd(J1{t1[0], t1[1], t1[2]}, d2);
-  if ((rc = msm_device<C, false>(ctx, a, pk->Z, n - 1, t1, true))) return rc;
+  if ((rc = msm_device<C, false>(ctx, a, pk->Z, n - 1, t1, true, pZ))) return rc;
   krs = host::jadd(krs, J1{t1[0], t1[1], t1[2]});
-  // Bs = MSM_G2(wB, B2) + s delta2 + beta2   (computeBS2 icicle.go:377-393)
-  HF2 t2[3];
-  if ((rc = msm_device<C, true>(ctx, wB.p, pk->B2, pk->nbB, t2, true))) return rc;
   cross.join();
   krs = host::jadd(krs, s_ar);
   krs = host::jadd(krs, r_bs1);

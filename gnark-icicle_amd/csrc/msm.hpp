@@ -1,4 +1,4 @@
-// MSM entry points (see msm.hip).
+// MSM entry points (see msm_impl.hpp).
 #pragma once
 #include <cstddef>
 #include <cstdint>
@@ -11,17 +11,58 @@ struct Arena;
 // Sorts M (key, value) u32 pairs by the low end_bit key bits (msm_sort.hip).
 int msm_sort_pairs(gm_ctx* ctx, Arena& arena, const uint32_t* keys_in, uint32_t* keys_out,
                    const uint32_t* vals_in, uint32_t* vals_out, size_t M, int end_bit);
+
+// Fixed-base precomputation of a resident point set (a proving key's arrays):
+// W copies of the n points, copy w = [2^(c w)] P_i at index w * stride + i, so
+// every window's digits land in ONE shared set of 2^(c-1) buckets.  The
+// accumulation work is unchanged (one mixed add per non-zero digit), but the
+// bucket reduction runs once instead of W times, which lets c grow (fewer
+// windows).  c == 0 means plain points (no precomputation).
+struct MsmPrecomp {
+  uint32_t c = 0, W = 0;
+  size_t stride = 0;
+};
+
+// Window size and copy count for a precomputed set of n points of a
+// `bits`-bit scalar field: minimises n*W accumulation adds + ~3 adds per bucket.
+MsmPrecomp msm_choose_precomp(size_t n, int bits);
+
+// Sorted signed-digit plan of one scalar vector: depends only on the scalars
+// and the point layout, so MSMs that share scalars and layout (Groth16's G1 and
+// G2 B-MSMs, prove.go:217,293) sort once.  Buffers live in the caller's Arena.
+struct MsmPlan {
+  uint32_t c = 0, W = 0, nb = 0, total = 0;
+  uint32_t Wred = 0;  // windows reduced separately: W (plain) or 1 (shared buckets)
+  size_t n = 0, M = 0;
+  size_t npts = 0;    // points addressable through the plan (bounds check)
+  uint32_t* keys = nullptr;     // sorted bucket keys, M entries
+  uint32_t* vals = nullptr;     // point index | sign << 31, M entries
+  uint32_t* offsets = nullptr;  // total + 1 bucket start offsets
+};
+template <class C>
+int msm_plan(gm_ctx* ctx, Arena& arena, const void* scalars_dev, size_t n, const MsmPrecomp* pre,
+             MsmPlan& plan);
+template <class C, bool G2>
+int msm_run(gm_ctx* ctx, const MsmPlan& plan, const void* points_internal,
+            typename GroupSel<C, G2>::HF (&jac_out)[3]);
+
 // out = sum_i int(scalars[i]) * points[i] as a host Jacobian triple (X, Y, Z).
 // points_dev is gnark-layout affine points, or (points_internal) an array of
-// device-internal Affine<F> (radix-2^29 Montgomery) prepared by
-// msm_prepare_points (e.g. a device-resident proving key).
+// device-internal points prepared by msm_prepare_points /
+// msm_precompute_points (e.g. a device-resident proving key); `pre` describes a
+// precomputed set.
 template <class C, bool G2>
 int msm_device(gm_ctx* ctx, const void* scalars_dev, const void* points_dev, size_t n,
-               typename GroupSel<C, G2>::HF (&jac_out)[3], bool points_internal = false);
+               typename GroupSel<C, G2>::HF (&jac_out)[3], bool points_internal = false,
+               const MsmPrecomp* pre = nullptr);
 // Converts n gnark-layout affine points into the internal layout (dst holds
 // n * msm_internal_point_bytes<C, G2>() bytes).
 template <class C, bool G2>
 int msm_prepare_points(gm_ctx* ctx, const void* gnark_points, size_t n, void* dst);
+// Same, plus the W - 1 shifted copies of `pre` (dst holds
+// pre.W * pre.stride * msm_internal_point_bytes<C, G2>() bytes, stride >= n).
+template <class C, bool G2>
+int msm_precompute_points(gm_ctx* ctx, const void* gnark_points, size_t n, const MsmPrecomp& pre, void* dst);
 template <class C, bool G2>
 size_t msm_internal_point_bytes();
 }  // namespace gm

@@ -3,4 +3,5 @@
 
 namespace gm {
 GM_MSM_INSTANTIATE(CurveBLS12377, false)
+GM_MSM_INSTANTIATE_PLAN(CurveBLS12377)
 }  // namespace gm

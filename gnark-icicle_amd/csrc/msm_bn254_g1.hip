@@ -3,4 +3,5 @@
 
 namespace gm {
 GM_MSM_INSTANTIATE(CurveBN254, false)
+GM_MSM_INSTANTIATE_PLAN(CurveBN254)
 }  // namespace gm

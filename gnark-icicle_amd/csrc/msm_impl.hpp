@@ -52,10 +52,12 @@ GM_DEV FeG<Fr> load_scalar_canonical(const uint32_t* __restrict__ s, uint32_t i)
 // Digit keys for a radix sort: key = global bucket index w*nb + |d|-1 (or the
 // sentinel `total` for a zero digit, which sorts past every bucket), value =
 // point index | sign << 31.  Window-major: entry (w, i) at w*n + i.
+// Precomputed (shared-bucket) layout: key = |d|-1 (sentinel nb) for every
+// window, value = index of the shifted copy, w*stride + i.
 template <class Fr>
 __global__ void __launch_bounds__(256) k_msm_keys(const uint32_t* __restrict__ scalars, uint32_t n,
-                                                  uint32_t c, uint32_t W, uint32_t* __restrict__ keys,
-                                                  uint32_t* __restrict__ vals) {
+                                                  uint32_t c, uint32_t W, uint32_t shared_stride,
+                                                  uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const FeG<Fr> k = load_scalar_canonical<Fr>(scalars, i);
@@ -74,8 +76,13 @@ __global__ void __launch_bounds__(256) k_msm_keys(const uint32_t* __restrict__ s
       neg = 0;
     }
     const size_t e = (size_t)w * n + i;
-    keys[e] = d ? w * nb + d - 1 : total;
-    vals[e] = i | (neg << 31);
+    if (shared_stride) {
+      keys[e] = d ? d - 1 : nb;
+      vals[e] = (w * shared_stride + i) | (neg << 31);
+    } else {
+      keys[e] = d ? w * nb + d - 1 : total;
+      vals[e] = i | (neg << 31);
+    }
   }
 }
 
@@ -89,6 +96,40 @@ __global__ void __launch_bounds__(256) k_msm_convert_points(const uint32_t* __re
   if (i >= n) return;
   constexpr int PW = 2 * Coord<F>::WORDS;
   store_affine_packed<F>(dst + i * PW, load_affine_gnark<F>(src + i * PW));
+}
+
+// Fixed-base copies: pts[w*stride + i] = [2^(c w)] pts[i] for w = 1..W-1
+// (copy 0 already converted).  c doublings per copy in XYZZ, then one Fermat
+// inversion back to affine; one-time setup cost, like the pk upload itself.
+template <class F>
+__global__ void __launch_bounds__(128) k_msm_precompute(uint32_t* __restrict__ pts, size_t n, size_t stride,
+                                                        uint32_t c, uint32_t W) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  constexpr int PW = 2 * Coord<F>::WORDS;
+  const Affine<F> P = load_affine_packed<F>(pts + i * PW);
+  Affine<F> zero;
+  zero.x = FOps<F>::zero();
+  zero.y = FOps<F>::zero();
+  if (aff_is_inf(P)) {
+    for (uint32_t w = 1; w < W; w++) store_affine_packed<F>(pts + (w * stride + i) * PW, zero);
+    return;
+  }
+  XYZZ<F> acc;
+  acc.x = P.x;
+  acc.y = P.y;
+  acc.zz = FOps<F>::one();
+  acc.zzz = FOps<F>::one();
+  for (uint32_t w = 1; w < W; w++) {
+    for (uint32_t k = 0; k < c; k++) acc = xyzz_dbl(acc);
+    Affine<F> r = zero;
+    if (!xyzz_is_inf(acc)) {
+      const F t = fe_inv(fe_mul(acc.zz, acc.zzz));
+      r.x = fe_mul(acc.x, fe_mul(t, acc.zzz));  // X / ZZ
+      r.y = fe_mul(acc.y, fe_mul(t, acc.zz));   // Y / ZZZ
+    }
+    store_affine_packed<F>(pts + (w * stride + i) * PW, r);
+  }
 }
 
 // raw words of one packed point (vector loads; unpacked just before use)
@@ -408,83 +449,106 @@ static int choose_window(size_t n, int bits) {
   return best;
 }
 
+// Keys, sort and bucket offsets for one scalar vector (see MsmPlan).
+template <class C>
+int msm_plan(gm_ctx* ctx, Arena& arena, const void* scalars_dev, size_t n, const MsmPrecomp* pre,
+             MsmPlan& plan) {
+  hipStream_t st = ctx->stream;
+  plan = MsmPlan();
+  plan.n = n;
+  if (n == 0) return GM_OK;
+  if (n >= (size_t(1) << 31)) {
+    set_error("msm: n must be < 2^31");
+    return GM_ERR_INVALID;
+  }
+  const bool shared = pre && pre->c;
+  if (shared && (pre->stride < n || (size_t)pre->W * pre->stride >= (size_t(1) << 31) ||
+                 (size_t)pre->c * pre->W < (size_t)C::FR_BITS + 1)) {
+    set_error("msm: precomputed point set does not cover this MSM");
+    return GM_ERR_INVALID;
+  }
+  const uint32_t c = shared ? pre->c
+                            : (ctx->msm_c_override ? (uint32_t)ctx->msm_c_override
+                                                   : (uint32_t)choose_window(n, C::FR_BITS));
+  // ceil((bits+1)/c): the top signed digit never carries
+  const uint32_t W = shared ? pre->W : (C::FR_BITS + 1 + c - 1) / c;
+  plan.c = c;
+  plan.W = W;
+  plan.nb = 1u << (c - 1);
+  plan.Wred = shared ? 1 : W;
+  plan.total = plan.Wred * plan.nb;
+  plan.npts = shared ? (size_t)W * pre->stride : n;
+  const size_t M = (size_t)W * n;
+  plan.M = M;
+  if (M >= (size_t(1) << 31)) {
+    set_error("msm: n * windows must be < 2^31");
+    return GM_ERR_INVALID;
+  }
+  int rc;
+  DevBuf keys_in, vals_in, keys_out, vals_out, offsets;
+  if ((rc = keys_in.alloc(arena, sizeof(uint32_t) * M)) || (rc = vals_in.alloc(arena, sizeof(uint32_t) * M)) ||
+      (rc = keys_out.alloc(arena, sizeof(uint32_t) * M)) || (rc = vals_out.alloc(arena, sizeof(uint32_t) * M)) ||
+      (rc = offsets.alloc(arena, sizeof(uint32_t) * (plan.total + 1))))
+    return rc;
+  {
+    ProfScope ps(ctx, "msm_keys");
+    hipLaunchKernelGGL(k_msm_keys<typename C::Fr>, dim3(blocks_for(n, 256)), dim3(256), 0, st,
+                       reinterpret_cast<const uint32_t*>(scalars_dev), (uint32_t)n, c, W,
+                       shared ? (uint32_t)pre->stride : 0u, keys_in.as<uint32_t>(), vals_in.as<uint32_t>());
+  }
+  GM_HIP(hipGetLastError());
+  int end_bit = 1;
+  while ((1ull << end_bit) <= plan.total) end_bit++;
+  {
+    ProfScope ps(ctx, "msm_sort");
+    if ((rc = msm_sort_pairs(ctx, arena, keys_in.as<uint32_t>(), keys_out.as<uint32_t>(), vals_in.as<uint32_t>(),
+                             vals_out.as<uint32_t>(), M, end_bit)))
+      return rc;
+  }
+  {
+    ProfScope ps(ctx, "msm_offsets");
+    hipLaunchKernelGGL(k_msm_lower_bound, dim3(blocks_for((size_t)plan.total + 1, 256)), dim3(256), 0, st,
+                       keys_out.as<uint32_t>(), (uint32_t)M, plan.total, offsets.as<uint32_t>());
+  }
+  GM_HIP(hipGetLastError());
+  plan.keys = keys_out.as<uint32_t>();
+  plan.vals = vals_out.as<uint32_t>();
+  plan.offsets = offsets.as<uint32_t>();
+  return GM_OK;
+}
+
+// Bucket accumulation, reduction and the host Horner tail over a plan.
 template <class C, bool G2>
-int msm_device(gm_ctx* ctx, const void* scalars_dev, const void* points_dev, size_t n,
-               typename GroupSel<C, G2>::HF (&jac_out)[3], bool points_internal) {
+int msm_run(gm_ctx* ctx, const MsmPlan& plan, const void* points_internal,
+            typename GroupSel<C, G2>::HF (&jac_out)[3]) {
   using DF = typename GroupSel<C, G2>::DF;
   using HF = typename GroupSel<C, G2>::HF;
   using HJ = host::Jac<HF>;
   hipStream_t st = ctx->stream;
-  if (n == 0) {
+  if (plan.n == 0) {
     HJ inf = HJ::inf();
     jac_out[0] = inf.x;
     jac_out[1] = inf.y;
     jac_out[2] = inf.z;
     return GM_OK;
   }
-  if (n >= (size_t(1) << 31)) {
-    set_error("msm: n must be < 2^31");
-    return GM_ERR_INVALID;
-  }
-  const uint32_t c = ctx->msm_c_override ? (uint32_t)ctx->msm_c_override : (uint32_t)choose_window(n, C::FR_BITS);
-  const uint32_t W = (C::FR_BITS + 1 + c - 1) / c;  // ceil((bits+1)/c): top signed digit never carries
-  const uint32_t nb = 1u << (c - 1);
-  const uint32_t total = W * nb;
+  const uint32_t c = plan.c, nb = plan.nb, total = plan.total, Wr = plan.Wred;
+  const size_t M = plan.M;
   const uint32_t L = nb >= 4 ? 4 : nb;  // level-1 segment length (buckets)
   const uint32_t nseg = nb / L;
   int rc;
 
   Arena arena(ctx);
   constexpr int WORDS = Coord<DF>::WORDS;  // u32 words of one gnark-layout coordinate
-  DevBuf counts, offsets, sorted, buckets, nodes_a, nodes_b, wsum, errw, ipts, keys_in, keys_out;
+  DevBuf buckets, nodes_a, nodes_b, wsum, errw;
   if ((rc = errw.alloc(arena, 16))) return rc;
   GM_HIP(hipMemsetAsync(errw.p, 0, 16, st));
-  // counts doubles as the unsorted value array of the radix sort
-  if ((rc = counts.alloc(arena, sizeof(uint32_t) * (size_t)W * n))) return rc;
-  if ((rc = keys_in.alloc(arena, sizeof(uint32_t) * (size_t)W * n))) return rc;
-  if ((rc = keys_out.alloc(arena, sizeof(uint32_t) * (size_t)W * n))) return rc;
-  if ((rc = offsets.alloc(arena, sizeof(uint32_t) * (total + 1)))) return rc;
-  if ((rc = sorted.alloc(arena, sizeof(uint32_t) * (size_t)W * n))) return rc;
   if ((rc = buckets.alloc(arena, sizeof(XYZZ<DF>) * (size_t)total))) return rc;
-  if ((rc = nodes_a.alloc(arena, sizeof(XYZZ<DF>) * 2 * (size_t)W * nseg))) return rc;
-  if ((rc = nodes_b.alloc(arena, sizeof(XYZZ<DF>) * 2 * (size_t)W * nseg))) return rc;
-  if ((rc = wsum.alloc(arena, sizeof(uint32_t) * 4 * WORDS * W * (2 + c)))) return rc;
-  constexpr size_t PTB = 2 * WORDS * sizeof(uint32_t);  // packed point bytes
-  const uint32_t* pts_internal = reinterpret_cast<const uint32_t*>(points_dev);
-  if (!points_internal) {
-    if ((rc = ipts.alloc(arena, PTB * n))) return rc;
-    ProfScope ps(ctx, "msm_convert_points");
-    hipLaunchKernelGGL(k_msm_convert_points<DF>, dim3(blocks_for(n, 256)), dim3(256), 0, st,
-                       reinterpret_cast<const uint32_t*>(points_dev), n, ipts.as<uint32_t>());
-    pts_internal = ipts.as<uint32_t>();
-  }
-
-  const uint32_t* sc = reinterpret_cast<const uint32_t*>(scalars_dev);
-  const size_t M = (size_t)W * n;
-  if (M >= (size_t(1) << 31)) {
-    set_error("msm: n * windows must be < 2^31");
-    return GM_ERR_INVALID;
-  }
-  {
-    ProfScope ps(ctx, "msm_keys");
-    hipLaunchKernelGGL(k_msm_keys<typename C::Fr>, dim3(blocks_for(n, 256)), dim3(256), 0, st, sc,
-                       (uint32_t)n, c, W, keys_in.as<uint32_t>(), counts.as<uint32_t>());
-  }
-  GM_HIP(hipGetLastError());
-  int end_bit = 1;
-  while ((1ull << end_bit) <= total) end_bit++;
-  {
-    ProfScope ps(ctx, "msm_sort");
-    if ((rc = msm_sort_pairs(ctx, arena, keys_in.as<uint32_t>(), keys_out.as<uint32_t>(), counts.as<uint32_t>(),
-                             sorted.as<uint32_t>(), M, end_bit)))
-      return rc;
-  }
-  {
-    ProfScope ps(ctx, "msm_offsets");
-    hipLaunchKernelGGL(k_msm_lower_bound, dim3(blocks_for((size_t)total + 1, 256)), dim3(256), 0, st,
-                       keys_out.as<uint32_t>(), (uint32_t)M, total, offsets.as<uint32_t>());
-  }
-  GM_HIP(hipGetLastError());
+  if ((rc = nodes_a.alloc(arena, sizeof(XYZZ<DF>) * 2 * (size_t)Wr * nseg))) return rc;
+  if ((rc = nodes_b.alloc(arena, sizeof(XYZZ<DF>) * 2 * (size_t)Wr * nseg))) return rc;
+  if ((rc = wsum.alloc(arena, sizeof(uint32_t) * 4 * WORDS * Wr * (2 + c)))) return rc;
+  const uint32_t* pts_internal = reinterpret_cast<const uint32_t*>(points_internal);
+  const uint32_t* offsets = plan.offsets;
   {
     const uint32_t K = ctx->msm_slice ? (uint32_t)ctx->msm_slice : 64u;
     const size_t nslices = (M + K - 1) / K;
@@ -500,30 +564,27 @@ int msm_device(gm_ctx* ctx, const void* scalars_dev, const void* points_dev, siz
     if (ov && !strcmp(ov, "noprefetch")) noprefetch = true;
     auto accum = noprefetch ? k_msm_accum_seg_g2<DF> : k_msm_accum_seg<DF>;
     hipLaunchKernelGGL(accum, dim3(blocks_for(nslices, 128)), dim3(128), 0, st, pts_internal,
-                       (uint32_t)n, keys_out.as<uint32_t>(), sorted.as<uint32_t>(), offsets.as<uint32_t>(), total,
-                       K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>(),
-                       errw.as<uint32_t>());
-    hipLaunchKernelGGL(k_msm_fixup<DF>, dim3(blocks_for(total, 128)), dim3(128), 0, st, offsets.as<uint32_t>(),
-                       total, K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>(),
+                       (uint32_t)plan.npts, plan.keys, plan.vals, offsets, total, K, buckets.as<XYZZ<DF>>(),
+                       pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>(), errw.as<uint32_t>());
+    hipLaunchKernelGGL(k_msm_fixup<DF>, dim3(blocks_for(total, 128)), dim3(128), 0, st, offsets, total, K,
+                       buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>(),
                        errw.as<uint32_t>() + 1);
     uint32_t maxspan = 0;
     GM_HIP(hipMemcpyAsync(&maxspan, errw.as<uint32_t>() + 1, 4, hipMemcpyDeviceToHost, st));
     GM_HIP(hipStreamSynchronize(st));
     if (maxspan > FIX_SERIAL) {
       for (uint32_t d = 0; (1u << d) < maxspan; d++)
-        hipLaunchKernelGGL(k_msm_fix_tree<DF>, dim3(blocks_for(nslices, 128)), dim3(128), 0, st,
-                           keys_out.as<uint32_t>(), offsets.as<uint32_t>(), total, K, (uint32_t)nslices, d,
-                           pfirst.as<XYZZ<DF>>());
-      hipLaunchKernelGGL(k_msm_fixup_long<DF>, dim3(blocks_for(total, 128)), dim3(128), 0, st,
-                         offsets.as<uint32_t>(), total, K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(),
-                         plast.as<XYZZ<DF>>());
+        hipLaunchKernelGGL(k_msm_fix_tree<DF>, dim3(blocks_for(nslices, 128)), dim3(128), 0, st, plan.keys,
+                           offsets, total, K, (uint32_t)nslices, d, pfirst.as<XYZZ<DF>>());
+      hipLaunchKernelGGL(k_msm_fixup_long<DF>, dim3(blocks_for(total, 128)), dim3(128), 0, st, offsets, total,
+                         K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>());
     }
   }
   uint32_t Q = 2;  // points per node: [G, U, Y_0..Y_{Q-3}]
   {
     ProfScope ps(ctx, "msm_bucket_reduce");
-    hipLaunchKernelGGL(k_msm_seg<DF>, dim3(blocks_for((size_t)W * nseg, 128)), dim3(128), 0, st,
-                       buckets.as<XYZZ<DF>>(), nb, L, nseg, W, nodes_a.as<XYZZ<DF>>());
+    hipLaunchKernelGGL(k_msm_seg<DF>, dim3(blocks_for((size_t)Wr * nseg, 128)), dim3(128), 0, st,
+                       buckets.as<XYZZ<DF>>(), nb, L, nseg, Wr, nodes_a.as<XYZZ<DF>>());
     // LDS tree levels until one node per window
     constexpr size_t SLOT_BUDGET = (96u << 10) / sizeof(XYZZ<DF>);
     uint32_t m = nseg;
@@ -539,21 +600,21 @@ int msm_device(gm_ctx* ctx, const void* scalars_dev, const void* points_dev, siz
       }
       const uint32_t NT = 1u << lg;
       const uint32_t groups = m / NT;
-      hipLaunchKernelGGL(k_msm_bitsum<DF>, dim3(W * groups), dim3(256), sizeof(XYZZ<DF>) * NT * Q, st, cur, m,
+      hipLaunchKernelGGL(k_msm_bitsum<DF>, dim3(Wr * groups), dim3(256), sizeof(XYZZ<DF>) * NT * Q, st, cur, m,
                          Q, NT, lg, nxt);
       Q += lg;
       m = groups;
       std::swap(cur, nxt);
     }
-    hipLaunchKernelGGL(k_msm_export<DF>, dim3(blocks_for((size_t)W * Q, 128)), dim3(128), 0, st, cur, W * Q,
+    hipLaunchKernelGGL(k_msm_export<DF>, dim3(blocks_for((size_t)Wr * Q, 128)), dim3(128), 0, st, cur, Wr * Q,
                        wsum.as<uint32_t>());
   }
   GM_HIP(hipGetLastError());
   uint32_t herr = 0;
   GM_HIP(hipMemcpyAsync(&herr, errw.p, 4, hipMemcpyDeviceToHost, st));
-  std::vector<HF> hw(4 * (size_t)W * Q);
+  std::vector<HF> hw(4 * (size_t)Wr * Q);
   static_assert(sizeof(HF) == 4 * WORDS, "host/device layout mismatch");
-  GM_HIP(hipMemcpyAsync(hw.data(), wsum.p, sizeof(uint32_t) * 4 * WORDS * W * Q, hipMemcpyDeviceToHost, st));
+  GM_HIP(hipMemcpyAsync(hw.data(), wsum.p, sizeof(uint32_t) * 4 * WORDS * Wr * Q, hipMemcpyDeviceToHost, st));
   GM_HIP(hipStreamSynchronize(st));
   if (herr) {
     set_error("msm: internal consistency check failed (code " + std::to_string(herr) + ")");
@@ -561,12 +622,12 @@ int msm_device(gm_ctx* ctx, const void* scalars_dev, const void* points_dev, siz
   }
   // Host Horner over bit positions: window w contributes U_w at 2^(c w) and
   // Y_{w,b} at 2^(c w + log2 L + b) (b < Q - 2 = log2(nseg), so every exponent
-  // stays below c (w + 1)).
+  // stays below c (w + 1)).  Shared buckets: one window, w = 0.
   uint32_t lgL = 0;
   while ((1u << lgL) < L) lgL++;
-  const int top = (int)(c * W);
+  const int top = (int)(c * Wr);
   std::vector<std::vector<uint32_t>> at(top + 1);  // point ids per exponent
-  for (uint32_t w = 0; w < W; w++) {
+  for (uint32_t w = 0; w < Wr; w++) {
     at[c * w].push_back(w * Q + 1);
     for (uint32_t b = 0; b + 2 < Q; b++) at[c * w + lgL + b].push_back(w * Q + 2 + b);
   }
@@ -586,6 +647,30 @@ int msm_device(gm_ctx* ctx, const void* scalars_dev, const void* points_dev, siz
 }
 
 template <class C, bool G2>
+int msm_device(gm_ctx* ctx, const void* scalars_dev, const void* points_dev, size_t n,
+               typename GroupSel<C, G2>::HF (&jac_out)[3], bool points_internal, const MsmPrecomp* pre) {
+  using DF = typename GroupSel<C, G2>::DF;
+  Arena arena(ctx);
+  int rc;
+  const void* pts = points_dev;
+  DevBuf ipts;
+  if (!points_internal && n) {
+    if (pre && pre->c) {
+      set_error("msm: a precomputed point set must be device-internal");
+      return GM_ERR_INVALID;
+    }
+    if ((rc = ipts.alloc(arena, 2 * Coord<DF>::WORDS * sizeof(uint32_t) * n))) return rc;
+    ProfScope ps(ctx, "msm_convert_points");
+    hipLaunchKernelGGL(k_msm_convert_points<DF>, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream,
+                       reinterpret_cast<const uint32_t*>(points_dev), n, ipts.as<uint32_t>());
+    pts = ipts.p;
+  }
+  MsmPlan plan;
+  if ((rc = msm_plan<C>(ctx, arena, scalars_dev, n, pre, plan))) return rc;
+  return msm_run<C, G2>(ctx, plan, pts, jac_out);
+}
+
+template <class C, bool G2>
 size_t msm_internal_point_bytes() {
   return 2 * Coord<typename GroupSel<C, G2>::DF>::WORDS * sizeof(uint32_t);
 }
@@ -600,12 +685,34 @@ int msm_prepare_points(gm_ctx* ctx, const void* gnark_points, size_t n, void* ds
   return GM_OK;
 }
 
+template <class C, bool G2>
+int msm_precompute_points(gm_ctx* ctx, const void* gnark_points, size_t n, const MsmPrecomp& pre, void* dst) {
+  using DF = typename GroupSel<C, G2>::DF;
+  if (n == 0) return GM_OK;
+  if (pre.stride < n || pre.W == 0 || pre.c == 0) {
+    set_error("msm precompute: bad layout");
+    return GM_ERR_INVALID;
+  }
+  hipLaunchKernelGGL(k_msm_convert_points<DF>, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream,
+                     reinterpret_cast<const uint32_t*>(gnark_points), n, reinterpret_cast<uint32_t*>(dst));
+  if (pre.W > 1)
+    hipLaunchKernelGGL(k_msm_precompute<DF>, dim3(blocks_for(n, 128)), dim3(128), 0, ctx->stream,
+                       reinterpret_cast<uint32_t*>(dst), n, pre.stride, pre.c, pre.W);
+  GM_HIP(hipGetLastError());
+  return GM_OK;
+}
+
 // Explicit instantiation for one (curve, group); each lives in its own
 // translation unit (msm_<curve>_<group>.hip) so the four compile in parallel.
+// The scalar-only plan is instantiated with the G1 unit.
 #define GM_MSM_INSTANTIATE(C, G2)                                                              \
   template size_t msm_internal_point_bytes<C, G2>();                                          \
   template int msm_prepare_points<C, G2>(gm_ctx*, const void*, size_t, void*);                \
+  template int msm_precompute_points<C, G2>(gm_ctx*, const void*, size_t, const MsmPrecomp&, void*); \
+  template int msm_run<C, G2>(gm_ctx*, const MsmPlan&, const void*, typename GroupSel<C, G2>::HF (&)[3]); \
   template int msm_device<C, G2>(gm_ctx*, const void*, const void*, size_t,                    \
-                                 typename GroupSel<C, G2>::HF (&)[3], bool);
+                                 typename GroupSel<C, G2>::HF (&)[3], bool, const MsmPrecomp*);
+#define GM_MSM_INSTANTIATE_PLAN(C) \
+  template int msm_plan<C>(gm_ctx*, Arena&, const void*, size_t, const MsmPrecomp*, MsmPlan&);
 
 }  // namespace gm

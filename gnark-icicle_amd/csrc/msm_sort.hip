@@ -20,4 +20,23 @@ int msm_sort_pairs(gm_ctx* ctx, Arena& arena, const uint32_t* keys_in, uint32_t*
   return GM_OK;
 }
 
+// Shared-bucket cost model: n*W accumulation adds + ~3 reduction adds per
+// bucket, paid once (not per window).  Picks c = 20 / W = 13 for 2^20 BN254
+// points and c = 22 / W = 12 for 2^24.
+MsmPrecomp msm_choose_precomp(size_t n, int bits) {
+  MsmPrecomp best;
+  double best_cost = 1e300;
+  for (uint32_t c = 8; c <= 24; c++) {
+    const uint32_t W = (uint32_t)((bits + 1 + c - 1) / c);
+    const double cost = (double)n * W + 3.0 * (double)(1u << (c - 1));
+    if (cost < best_cost) {
+      best_cost = cost;
+      best.c = c;
+      best.W = W;
+    }
+  }
+  best.stride = n;
+  return best;
+}
+
 }  // namespace gm

@@ -40,8 +40,9 @@ SYMBOLS = [
     "gm_last_error", "gm_version", "gm_init", "gm_destroy", "gm_synchronize",
     "gm_profile_enable", "gm_profile_reset", "gm_profile_get", "gm_profile_dump",
     "gm_set_msm_window", "gm_malloc", "gm_free", "gm_copy_to_device", "gm_memcpy_h2d",
-    "gm_memcpy_d2h", "gm_memcpy_d2d", "gm_copy_points_to_device", "gm_msm", "gm_msm_host_scalars", "gm_points_upload", "gm_msm_prepared", "gm_kzg_commit", "gm_ntt",
-    "gm_poly_ops", "gm_reverse_scalars", "gm_groth16_compute_h", "gm_g16_pk_upload",
+    "gm_memcpy_d2h", "gm_memcpy_d2d", "gm_copy_points_to_device", "gm_msm", "gm_msm_host_scalars", "gm_points_upload", "gm_msm_prepared", "gm_precompute_layout", "gm_points_upload_precomputed",
+    "gm_msm_precomputed", "gm_kzg_commit", "gm_ntt",
+    "gm_poly_ops", "gm_reverse_scalars", "gm_groth16_compute_h", "gm_g16_pk_upload", "gm_g16_pk_upload_ex",
     "gm_g16_pk_free", "gm_g16_prove", "gm_g16_prove_device", "gm_jac_add", "gm_jac_to_affine",
     "gm_batch_mul_base", "gm_random_scalars", "gm_generator", "gm_test_field_op",
     "gm_test_point_op",
@@ -85,12 +86,16 @@ def load_library(path: str = LIB_PATH):
     L.gm_msm_host_scalars.argtypes = [vp, i, i, vp, vp, sz, vp, vp]
     L.gm_points_upload.argtypes = [vp, i, i, vp, sz, pvp]
     L.gm_msm_prepared.argtypes = [vp, i, i, vp, vp, sz, vp, vp]
+    L.gm_precompute_layout.argtypes = [i, sz, i, ctypes.POINTER(i), ctypes.POINTER(i)]
+    L.gm_points_upload_precomputed.argtypes = [vp, i, i, vp, sz, i, pvp]
+    L.gm_msm_precomputed.argtypes = [vp, i, i, vp, vp, sz, i, sz, vp, vp]
     L.gm_kzg_commit.argtypes = [vp, i, vp, sz, vp, sz, vp]
     L.gm_ntt.argtypes = [vp, i, vp, sz, i, i, i]
     L.gm_poly_ops.argtypes = [vp, i, vp, vp, vp, sz, vp]
     L.gm_reverse_scalars.argtypes = [vp, i, vp, sz]
     L.gm_groth16_compute_h.argtypes = [vp, i, vp, vp, vp, sz, sz]
     L.gm_g16_pk_upload.argtypes = [vp, i, vp, pvp]
+    L.gm_g16_pk_upload_ex.argtypes = [vp, i, vp, ctypes.c_uint, pvp]
     L.gm_g16_pk_free.argtypes = [vp, vp]
     L.gm_g16_prove.argtypes = [vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, vp, vp]
     L.gm_g16_prove_device.argtypes = [vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, vp, vp]
@@ -271,6 +276,25 @@ class Context:
                                               _p(jac), _p(aff)))
         return jac.tobytes(), aff.tobytes()
 
+    def points_upload_precomputed(self, curve, points, g2: bool = False, window: int = 0) -> DeviceBuffer:
+        """Point set plus its fixed-base window copies (gm_points_upload_precomputed)."""
+        a = _buf(points)
+        n = a.size // point_bytes(curve, g2)
+        p = ctypes.c_void_p()
+        _check(load_library().gm_points_upload_precomputed(self.handle, curve_id(curve), int(g2), _p(a), n, window,
+                                                           ctypes.byref(p)))
+        buf = DeviceBuffer(self, p.value, a.size)
+        buf.count = n
+        buf.window = window
+        return buf
+
+    def msm_precomputed(self, curve, scalars: DeviceBuffer, prepared: DeviceBuffer, n: int, g2: bool = False):
+        jac = np.zeros(jac_bytes(curve, g2), np.uint8)
+        aff = np.zeros(point_bytes(curve, g2), np.uint8)
+        _check(load_library().gm_msm_precomputed(self.handle, curve_id(curve), int(g2), scalars.ptr, prepared.ptr,
+                                                 prepared.count, prepared.window, n, _p(jac), _p(aff)))
+        return jac.tobytes(), aff.tobytes()
+
     def kzg_commit(self, curve, srs: DeviceBuffer, coeffs) -> bytes:
         """kzg.Commit(p, pk): G1 digest of the polynomial coefficients (host)."""
         c = _buf(coeffs)
@@ -446,7 +470,10 @@ class ProvingKey:
     commitments filter K, prove.go:243-245; default nb_public + i).
     """
 
-    def __init__(self, ctx: Context, curve, pk: dict, domain_size: int, nb_wires: int, nb_public: int):
+    PRECOMPUTE = 1  # GM_PK_PRECOMPUTE
+
+    def __init__(self, ctx: Context, curve, pk: dict, domain_size: int, nb_wires: int, nb_public: int,
+                 precompute: bool = False):
         self.ctx = ctx
         self.curve = curve_id(curve)
         g1b = point_bytes(curve, False)
@@ -466,7 +493,8 @@ class ProvingKey:
             arrs["k_wires"] = kw
         self._keep = arrs
         handle = ctypes.c_void_p()
-        _check(load_library().gm_g16_pk_upload(ctx.handle, self.curve, ctypes.byref(h), ctypes.byref(handle)))
+        _check(load_library().gm_g16_pk_upload_ex(ctx.handle, self.curve, ctypes.byref(h),
+                                                  self.PRECOMPUTE if precompute else 0, ctypes.byref(handle)))
         self.handle = handle
         self.n, self.nb_wires, self.nb_public = domain_size, nb_wires, nb_public
 

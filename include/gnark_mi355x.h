@@ -93,6 +93,20 @@ int gm_points_upload(gm_ctx* ctx, int curve, int g2, const void* host_points, si
 int gm_msm_prepared(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const void* prepared,
                     size_t n, void* out_jac, void* out_affine);
 
+/* Fixed-base precomputation (ICICLE's MSM precompute_factor idea, re-derived):
+ * besides the n points, W-1 copies [2^(c w)] P_i (w = 1..W-1) are stored, so
+ * every window's digits share one bucket set and the bucket reduction runs
+ * once instead of W times (and c can grow).  window = c in [2, 24], or 0 =
+ * automatic from n.  Memory: W x the plain prepared size.  The copy count W =
+ * ceil((r_bits + 1) / c) is reported by gm_precompute_layout.  An MSM over
+ * any prefix n <= prepared_n of the set passes the SAME prepared_n and window
+ * used at upload. */
+int gm_precompute_layout(int curve, size_t prepared_n, int window, int* c_out, int* copies_out);
+int gm_points_upload_precomputed(gm_ctx* ctx, int curve, int g2, const void* host_points, size_t n,
+                                 int window, void** prepared_out);
+int gm_msm_precomputed(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const void* prepared,
+                       size_t prepared_n, int window, size_t n, void* out_jac, void* out_affine);
+
 /* ---- KZG commitment (PLONK; backend/plonk/bls12-377/prove.go:312,460,718,
  *      1158-1168 call gnark-crypto kzg.Commit) ---------------------------------
  * digest = sum_i coeffs[i] * srs[i] over the first n points of a prepared SRS
@@ -158,6 +172,12 @@ typedef struct {
 } gm_g16_pk_host;
 
 int gm_g16_pk_upload(gm_ctx* ctx, int curve, const gm_g16_pk_host* pk, gm_g16_pk** out);
+/* flags: GM_PK_PRECOMPUTE keeps fixed-base window copies of every point array
+ * on the device (gm_points_upload_precomputed; ~12x the point memory at 2^24,
+ * ~77 GB for a BN254 2^24 key) -- fewer windows and one bucket reduction per
+ * MSM.  gm_g16_pk_upload(...) == gm_g16_pk_upload_ex(..., 0, ...). */
+#define GM_PK_PRECOMPUTE 1u
+int gm_g16_pk_upload_ex(gm_ctx* ctx, int curve, const gm_g16_pk_host* pk, unsigned flags, gm_g16_pk** out);
 int gm_g16_pk_free(gm_ctx* ctx, gm_g16_pk* pk);
 
 /* Proves with solved vectors in host memory: wires (nb_wires Fr), a, b, c

@@ -58,3 +58,18 @@ def test_host_helpers_without_gpu(lib):
             jac = gen + one  # (X, Y, Z=1)
             two = gm.jac_add(cname, g2, jac, jac)
             assert pyref.decode_point(c, gm.jac_to_affine(cname, g2, two), g2) == G.mul(G.generator(), 2)
+
+
+def test_precompute_layout_host_only(lib):
+    """gm_precompute_layout is pure host logic: window choice and copy count."""
+    c, w = ctypes.c_int(), ctypes.c_int()
+    lib.gm_precompute_layout.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
+                                         ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+    assert lib.gm_precompute_layout(0, 1 << 20, 0, ctypes.byref(c), ctypes.byref(w)) == 0
+    assert (c.value, w.value) == (20, 13)
+    assert lib.gm_precompute_layout(0, 1 << 24, 0, ctypes.byref(c), ctypes.byref(w)) == 0
+    assert (c.value, w.value) == (22, 12)
+    assert lib.gm_precompute_layout(1, 1000, 9, ctypes.byref(c), ctypes.byref(w)) == 0
+    assert (c.value, w.value) == (9, 29)   # ceil((253 + 1) / 9)
+    assert lib.gm_precompute_layout(0, 1000, 40, ctypes.byref(c), ctypes.byref(w)) != 0
+    assert lib.gm_precompute_layout(7, 1000, 0, ctypes.byref(c), ctypes.byref(w)) != 0

@@ -18,7 +18,7 @@ TOXIC = [0x1D5A2B3C4D5E6F708192A3B4C5D6E7F8091A2B3C4D5E6F708192A3B4C5D6E7,
          0x1B9E6F708192A3B4C5D6E7F8091A2B3C4D5E6F708192A3B4C5D6E7F8091A2B]
 
 
-def _prove_both(gm_ctx, oracle, cname, r1, W, rr, ss):
+def _prove_both(gm_ctx, oracle, cname, r1, W, rr, ss, precompute=False):
     import gnark_mi355x as gm
     c = pyref.CURVES[cname]
     tox = R.encode_vec(cname, [t % c.r for t in TOXIC])
@@ -27,7 +27,7 @@ def _prove_both(gm_ctx, oracle, cname, r1, W, rr, ss):
     enc = lambda v: R.encode_vec(cname, v)
     rb, sb = enc([rr]), enc([ss])
     exp = oracle.g16_prove(cname, pk, r1.nb_public, enc(W), enc(a), enc(b), enc(cc), rb, sb)
-    dpk = gm.ProvingKey(gm_ctx, cname, pk, r1.domain_size, r1.nb_wires, r1.nb_public)
+    dpk = gm.ProvingKey(gm_ctx, cname, pk, r1.domain_size, r1.nb_wires, r1.nb_public, precompute=precompute)
     try:
         got = dpk.prove(enc(W), enc(a), enc(b), enc(cc), rb, sb)
     finally:
@@ -51,6 +51,16 @@ def test_groth16_squaring_chain(gm_ctx, oracle, cname, k):
     """refCircuit of backend/groth16/groth16_test.go:120-156 with k squarings."""
     r1, W = R.squaring_chain(k, cname, x=2)
     exp, got, ok = _prove_both(gm_ctx, oracle, cname, r1, W, 0xABCDEF0123, 0x13579BDF)
+    assert got == exp
+    assert ok == 7
+
+
+@pytest.mark.parametrize("cname,k", [("bn254", 15), ("bn254", 4000), ("bls12377", 511)])
+def test_groth16_precomputed_pk(gm_ctx, oracle, cname, k):
+    """GM_PK_PRECOMPUTE (fixed-base window copies of every pk array): the proof
+    is byte-identical to the CPU restatement."""
+    r1, W = R.squaring_chain(k, cname, x=3)
+    exp, got, ok = _prove_both(gm_ctx, oracle, cname, r1, W, 0x2468ACE, 0x1357BDF, precompute=True)
     assert got == exp
     assert ok == 7
 

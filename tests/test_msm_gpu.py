@@ -180,3 +180,61 @@ def test_kzg_commit_and_prepared_msm(gm_ctx, oracle, cname):
     assert gm_ctx.msm_prepared(cname, S, srs, m)[1] == gm_ctx.msm(cname, S, P, m)[1]
     for b in (S, P, srs):
         b.free()
+
+
+@pytest.mark.parametrize("cname,g2", CASES)
+def test_msm_precomputed_edge_vs_pyref(gm_ctx, cname, g2):
+    """Fixed-base precomputed set (W window copies, one shared bucket set): the
+    same edge inputs as the plain MSM, several windows, prefixes n <= prepared_n."""
+    c = pyref.CURVES[cname]
+    n = 48
+    sc, pts = _edge_inputs(cname, g2, n, 3000 + 7 * g2)
+    G = pyref.Group(c, g2)
+    sb = b"".join(pyref.encode_fr(c, s) for s in sc)
+    pb = b"".join(pyref.encode_point(c, p, g2) for p in pts)
+    S = gm_ctx.copy_to_device(sb)
+    for window in (0, 5, 9, 16):
+        pre = gm_ctx.points_upload_precomputed(cname, pb, g2, window)
+        for m in (n, 29, 1, 0):
+            _, aff = gm_ctx.msm_precomputed(cname, S, pre, m, g2)
+            exp = G.msm(sc[:m], pts[:m])
+            assert pyref.decode_point(c, aff, g2) == exp, (cname, g2, window, m)
+        pre.free()
+    S.free()
+
+
+@pytest.mark.parametrize("cname,g2,logn", [("bn254", False, 16), ("bn254", True, 12),
+                                           ("bls12377", False, 14), ("bls12377", True, 11)])
+def test_msm_precomputed_random_vs_oracle(gm_ctx, oracle, cname, g2, logn):
+    import gnark_mi355x as gm
+    n = (1 << logn) + 37
+    S = gm_ctx.random_scalars(cname, n, seed=0x5EED0005 + logn)
+    K = gm_ctx.random_scalars(cname, n, seed=0x5EED1005 + logn)
+    P = gm_ctx.batch_mul_base(cname, g2, gm.generator(cname, g2), K, n)
+    sb, pb = S.to_host(), P.to_host()
+    pre = gm_ctx.points_upload_precomputed(cname, pb, g2, 0)
+    _, aff = gm_ctx.msm_precomputed(cname, S, pre, n, g2)
+    assert aff == oracle.msm(cname, g2, sb, pb)
+    # skewed wire-like scalars: huge shared buckets (long-span fixup)
+    c = pyref.CURVES[cname]
+    rng = np.random.default_rng(logn)
+    table = np.frombuffer(b"".join(pyref.encode_fr(c, v) for v in (0, 1, 2, c.r - 1)), np.uint8).reshape(4, 32)
+    sk = table[rng.integers(0, 4, n)].tobytes()
+    S2 = gm_ctx.copy_to_device(sk)
+    _, aff = gm_ctx.msm_precomputed(cname, S2, pre, n, g2)
+    assert aff == oracle.msm(cname, g2, sk, pb)
+    for b in (S, S2, K, P, pre):
+        b.free()
+
+
+def test_msm_precomputed_large_matches_plain(gm_ctx):
+    """2^20 BN254 G1 (the bench workload): precomputed == plain, bit-exact."""
+    import gnark_mi355x as gm
+    n = 1 << 20
+    S = gm_ctx.random_scalars("bn254", n, seed=0x5EED0002)
+    K = gm_ctx.random_scalars("bn254", n, seed=0x5EED1002)
+    P = gm_ctx.batch_mul_base("bn254", False, gm.generator("bn254"), K, n)
+    pre = gm_ctx.points_upload_precomputed("bn254", P.to_host(), False, 0)
+    assert gm_ctx.msm_precomputed("bn254", S, pre, n)[1] == gm_ctx.msm("bn254", S, P, n)[1]
+    for b in (S, K, P, pre):
+        b.free()
