@@ -29,8 +29,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (8.0 TB/s spec)
 MSM_BYTES_PER_POINT = 96  # 64 B affine point + 32 B scalar
 # radix-2^29 BN254 Fp (9 limbs): mul = 2*81 mads, sqr = 45 + 81; mixed add = 8M + 2S
 MADS_PER_MIXED_ADD = 8 * 162 + 2 * 126
-# measured v_mad_u64_u32 issue peak (tools/microbench/mulos.hip: 125.6 Gmul/s x 162)
-MAD_PEAK_T = 20.3
+# measured v_mad_u64_u32 issue peak: 5.12 cycles per wave64 instruction per SIMD with
+# 8 independent chains at 8 waves/SIMD (tools/microbench/isa_rate.hip,
+# profiles/r01_isa_rate.txt): 1024 SIMDs x 64 lanes x 2.4 GHz / 5.12 = 30.7 T/s
+MAD_PEAK_T = 1024 * 64 * 2.4e9 / 5.12 / 1e12
 NTT_BYTES_PER_ELEM = 64   # one 32 B read + one 32 B write per transform
 
 
@@ -132,11 +134,12 @@ def main():
         "traffic": load_pmc_traffic("k_msm_accum_seg"),
         "avg_launch_ms": round(acc_avg_ms, 4),
         "bytes_per_launch": alg_bytes,
-        "int_alu": {"achieved": round(tmads, 3), "peak": MAD_PEAK_T, "unit": "T v_mad_u64_u32/s",
+        "int_alu": {"achieved": round(tmads, 3), "peak": round(MAD_PEAK_T, 2), "unit": "T v_mad_u64_u32/s",
                     "frac": round(tmads / MAD_PEAK_T, 4),
                     "work": "%d points x %d windows XYZZ mixed adds x %d mads" % (n, windows, MADS_PER_MIXED_ADD)},
-        "note": "MSM bucket accumulation is bound by 32-bit integer multiply issue (no MFMA, no HBM pressure): "
-                "int_alu is the binding roofline (DESIGN.md section 3)",
+        "note": "MSM bucket accumulation is bound by VALU issue (v_mad_u64_u32 plus the carry/mask "
+                "instructions of the radix-2^29 products; no MFMA, HBM well below peak): int_alu is the binding "
+                "roofline, priced at the measured mad-only issue peak (DESIGN.md section 3)",
     }
     kernel_ms = {k: round(v[0] / max(v[1], 1), 4) for k, v in stats.items()}
 

@@ -109,6 +109,53 @@ GM_DEV void xyzz_add_aff(XYZZ<F>& a, const Affine<F>& p) {
   a.x = X3;
 }
 
+// Lazily reduced a += p for G1 buckets (see field.hpp "Lazily reduced
+// arithmetic").  Invariants on a: x < 8p, y < 4p, zz < 2p, zzz < 2p (canonical
+// values qualify); p canonical.  Every product below has inputs with
+// ab <= 100 p^2 (largest: P^2 with P < 10p).  zz is never a non-zero multiple
+// of p (zz * PP with PP != 0 mod p), so fe_is_zero(zz) still tests infinity.
+template <class P>
+GM_DEV void xyzz_add_aff_lz(XYZZ<Fe<P>>& a, const Affine<Fe<P>>& p) {
+  static_assert(P::BITS + 7 <= RADIX * P::N, "lazy reduction needs R' > 128 p");
+  using F = Fe<P>;
+  if (aff_is_inf(p)) return;
+  if (xyzz_is_inf(a)) {
+    a.x = p.x;
+    a.y = p.y;
+    a.zz = fe_one<P>();
+    a.zzz = fe_one<P>();
+    return;
+  }
+  F Pd = fe_sub_lz<8>(fe_mul_lz(p.x, a.zz), a.x);   // U2 - X1   < 10p
+  F R = fe_sub_lz<4>(fe_mul_lz(p.y, a.zzz), a.y);   // S2 - Y1   < 6p
+  if (fe_is_zero_lz<10>(Pd)) {
+    if (fe_is_zero_lz<6>(R)) {
+      a = xyzz_dbl_aff(p);
+    } else {
+      a = xyzz_inf<F>();
+    }
+    return;
+  }
+  F PP = fe_sqr_lz(Pd);                              // < 2p
+  F PPP = fe_mul_lz(Pd, PP);                         // < 2p
+  a.zz = fe_mul_lz(a.zz, PP);
+  F Q = fe_mul_lz(a.x, PP);                          // < 2p
+  a.zzz = fe_mul_lz(a.zzz, PPP);
+  F X3 = fe_sub_lz<4>(fe_sub_lz<2>(fe_sqr_lz(R), PPP), fe_add_lz(Q, Q));  // < 8p
+  a.y = fe_sub_lz<2>(fe_mul_lz(R, fe_sub_lz<8>(Q, X3)), fe_mul_lz(a.y, PPP));  // R (<6p) * (<10p); < 4p
+  a.x = X3;
+}
+// canonical form of a lazily accumulated bucket
+template <class P>
+GM_DEV XYZZ<Fe<P>> xyzz_canon_lz(const XYZZ<Fe<P>>& a) {
+  XYZZ<Fe<P>> r;
+  r.x = fe_canon<3>(a.x);
+  r.y = fe_canon<2>(a.y);
+  r.zz = fe_canon<1>(a.zz);
+  r.zzz = fe_canon<1>(a.zzz);
+  return r;
+}
+
 // 2*a (dbl-2008-s-1, a = 0).  Infinity maps to infinity (ZZ3 = V*0).
 template <class F>
 GM_DEV XYZZ<F> xyzz_dbl(const XYZZ<F>& a) {

@@ -263,7 +263,7 @@ GM_DEV Fe<P> fe_neg(const Fe<P>& a) {
 // column k accumulates a_i b_{k-i} + m_i p_{k-i} (< 2N * 2^58 < 2^64) in one
 // 64-bit register; m_k = (acc * (-p^-1)) mod 2^29 zeroes the low limb.
 // Inputs < p  ->  result < 2p -> one conditional subtraction -> canonical.
-template <class P>
+template <class P, bool REDUCE = true>
 GM_DEV Fe<P> fe_mul(const Fe<P>& a, const Fe<P>& b) {
   constexpr int N = P::N;
   uint32_t m[N];
@@ -286,12 +286,12 @@ GM_DEV Fe<P> fe_mul(const Fe<P>& a, const Fe<P>& b) {
     acc >>= RADIX;
   }
   r.v[N - 1] = (uint32_t)acc;
-  fe_reduce_once(r);
+  if constexpr (REDUCE) fe_reduce_once(r);
   return r;
 }
 
 // Squaring: the symmetric products a_i a_j (i != j) are formed once and doubled.
-template <class P>
+template <class P, bool REDUCE = true>
 GM_DEV Fe<P> fe_sqr(const Fe<P>& a) {
   constexpr int N = P::N;
   uint32_t m[N];
@@ -319,8 +319,109 @@ GM_DEV Fe<P> fe_sqr(const Fe<P>& a) {
     acc >>= RADIX;
   }
   r.v[N - 1] = (uint32_t)acc;
-  fe_reduce_once(r);
+  if constexpr (REDUCE) fe_reduce_once(r);
   return r;
+}
+
+// ---------------------------------------------------------------------------
+// Lazily reduced arithmetic (MSM bucket accumulation hot loop).
+// Values are kept as representatives in [0, k p) with normalised 29-bit limbs
+// instead of canonical [0, p): the Montgomery product returns
+//   (ab + Mp) / R' < ab / R' + p,   M < R' = 2^(29N),
+// so with ab < R' p its output is already < 2p and the final conditional
+// subtraction (a third of the product's non-multiply instructions) can go.
+// fe_sub_lz<K> adds K p instead of testing the sign.  The accumulation keeps
+// x < 8p, y < 4p, zz, zzz < 2p and every product input pair satisfies
+// ab <= 100 p^2 < R' p, which needs R' / p > 100 (static_assert in the caller:
+// BITS + 7 <= 29 N, i.e. R' / p > 128; BN254 Fp: 254 + 7 = 261 = 29 * 9).
+// ---------------------------------------------------------------------------
+// limb i of K*p, normalised radix 2^29 (the top limb keeps any excess)
+template <class P, int K>
+GM_HD constexpr uint32_t kp_limb(int i) {
+  uint64_t carry = 0;
+  for (int j = 0; j < P::N; j++) {
+    const uint64_t v = (uint64_t)P::p(j) * K + carry;
+    if (j == i) return j == P::N - 1 ? (uint32_t)v : (uint32_t)(v & LIMB_MASK);
+    carry = v >> RADIX;
+  }
+  return 0;
+}
+// top limb of j*p (j < 16)
+template <class P>
+GM_HD constexpr uint32_t kp_top(int j) {
+  uint64_t carry = 0, v = 0;
+  for (int i = 0; i < P::N; i++) {
+    v = (uint64_t)P::p(i) * (uint64_t)j + carry;
+    carry = v >> RADIX;
+  }
+  return (uint32_t)v;
+}
+template <class P>
+GM_DEV Fe<P> fe_mul_lz(const Fe<P>& a, const Fe<P>& b) { return fe_mul<P, false>(a, b); }
+template <class P>
+GM_DEV Fe<P> fe_sqr_lz(const Fe<P>& a) { return fe_sqr<P, false>(a); }
+// a + b, no reduction (limbs normalised)
+template <class P>
+GM_DEV Fe<P> fe_add_lz(const Fe<P>& a, const Fe<P>& b) {
+  Fe<P> r;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < P::N; i++) {
+    const uint32_t s = a.v[i] + b.v[i] + c;
+    r.v[i] = i == P::N - 1 ? s : (s & LIMB_MASK);
+    c = s >> RADIX;
+  }
+  return r;
+}
+// a - b + K p  (requires b < K p; the result is < a + K p)
+template <int K, class P>
+GM_DEV Fe<P> fe_sub_lz(const Fe<P>& a, const Fe<P>& b) {
+  Fe<P> r;
+  int32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < P::N; i++) {
+    const int32_t d = (int32_t)(a.v[i] + kp_limb<P, K>(i)) - (int32_t)b.v[i] + c;
+    c = d >> RADIX;
+    r.v[i] = i == P::N - 1 ? (uint32_t)d : ((uint32_t)d & LIMB_MASK);
+  }
+  return r;
+}
+// a - K p if a >= K p
+template <int K, class P>
+GM_DEV void fe_reduce_k(Fe<P>& a) {
+  Fe<P> t;
+  int32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < P::N; i++) {
+    const int32_t d = (int32_t)a.v[i] - (int32_t)kp_limb<P, K>(i) + borrow;
+    borrow = d >> RADIX;
+    t.v[i] = (uint32_t)d & LIMB_MASK;
+  }
+  const bool ge = borrow == 0;
+#pragma unroll
+  for (int i = 0; i < P::N; i++) a.v[i] = ge ? t.v[i] : a.v[i];
+}
+// canonical representative of a < 2^L p (L <= 4)
+template <int L, class P>
+GM_DEV Fe<P> fe_canon(Fe<P> a) {
+  if constexpr (L >= 4) fe_reduce_k<8>(a);
+  if constexpr (L >= 3) fe_reduce_k<4>(a);
+  if constexpr (L >= 2) fe_reduce_k<2>(a);
+  if constexpr (L >= 1) fe_reduce_k<1>(a);
+  return a;
+}
+// Is a (< K p, K <= 16) congruent to 0?  a = j p forces a's top limb to be the
+// top limb of j p, so that cheap filter decides almost always; the exact test
+// runs only when the filter matches.
+template <int K, class P>
+GM_DEV bool fe_is_zero_lz(const Fe<P>& a) {
+  static_assert(K <= 16, "fe_canon<4> covers a < 16p");
+  const uint32_t top = a.v[P::N - 1];
+  bool hit = false;
+#pragma unroll
+  for (int j = 0; j < K; j++) hit |= top == kp_top<P>(j);
+  if (!hit) return false;
+  return fe_is_zero(fe_canon<4>(a));
 }
 
 // form conversions (see header comment)

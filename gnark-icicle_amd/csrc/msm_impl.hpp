@@ -158,11 +158,26 @@ GM_DEV PackedPt<PW> load_packed_pt(const uint32_t* __restrict__ src) {
 // edges go to part_first[t] / part_last[t] and are merged by k_msm_fixup.
 // Skewed scalar distributions (one huge bucket) therefore cost the same as
 // uniform ones in this phase.
+// G1 buckets accumulate lazily reduced (xyzz_add_aff_lz); G2 canonically.
 template <class F>
-GM_DEV void accum_emit(uint32_t b, const XYZZ<F>& acc, bool is_first, bool is_last, uint32_t start,
+struct LazyAcc {
+  static constexpr bool on = false;
+  GM_DEV static void add(XYZZ<F>& a, const Affine<F>& p) { xyzz_add_aff(a, p); }
+  GM_DEV static XYZZ<F> canon(const XYZZ<F>& a) { return a; }
+};
+template <class P>
+struct LazyAcc<Fe<P>> {
+  static constexpr bool on = true;
+  GM_DEV static void add(XYZZ<Fe<P>>& a, const Affine<Fe<P>>& p) { xyzz_add_aff_lz(a, p); }
+  GM_DEV static XYZZ<Fe<P>> canon(const XYZZ<Fe<P>>& a) { return xyzz_canon_lz(a); }
+};
+
+template <class F>
+GM_DEV void accum_emit(uint32_t b, const XYZZ<F>& acc_raw, bool is_first, bool is_last, uint32_t start,
                        uint32_t end, uint32_t t, const uint32_t* __restrict__ offsets,
                        XYZZ<F>* __restrict__ buckets, XYZZ<F>* __restrict__ part_first,
                        XYZZ<F>* __restrict__ part_last) {
+  const XYZZ<F> acc = LazyAcc<F>::canon(acc_raw);
   const uint32_t bs = offsets[b], be = offsets[b + 1];
   if (bs >= start && be <= end) {
     buckets[b] = acc;
@@ -220,7 +235,7 @@ GM_DEV void accum_seg_body(const uint32_t* __restrict__ points, uint32_t n,
     if (!PREFETCH) P = load_packed_pt<PW>(points + (size_t)(v & 0x7fffffffu) * PW);
     Affine<F> A = load_affine_packed<F>(P.w);
     if (v >> 31) A.y = fe_neg(A.y);
-    xyzz_add_aff(acc, A);
+    LazyAcc<F>::add(acc, A);
     if (PREFETCH) {
       v = vn;
       P = Pn;

@@ -238,3 +238,37 @@ def test_msm_precomputed_large_matches_plain(gm_ctx):
     assert gm_ctx.msm_precomputed("bn254", S, pre, n)[1] == gm_ctx.msm("bn254", S, P, n)[1]
     for b in (S, K, P, pre):
         b.free()
+
+
+@pytest.mark.parametrize("cname,g2", CASES)
+def test_msm_bucket_chain_special_cases(gm_ctx, cname, g2):
+    """Within one bucket the accumulator meets -(running sum) (-> infinity) and
+    +(running sum) (-> doubling) after several adds, i.e. while its coordinates
+    are non-canonical (lazily reduced G1 accumulation, field.hpp).  All scalars
+    are 1: every point lands in bucket 1 of window 0, accumulated in index order."""
+    c = pyref.CURVES[cname]
+    G = pyref.Group(c, g2)
+    base = pyref.random_points(c, 12, 4242 + g2, g2)
+    pts, run = [], None
+    for i, P in enumerate(base):
+        if i in (3, 9):
+            Q = G.neg(run)           # acc + (-acc) = infinity
+        elif i in (6,):
+            Q = run                  # acc + acc = doubling
+        else:
+            Q = P
+        pts.append(Q)
+        run = Q if run is None else G.add(run, Q)
+    n = len(pts)
+    sb = b"".join(pyref.encode_fr(c, 1) for _ in range(n))
+    pb = b"".join(pyref.encode_point(c, p, g2) for p in pts)
+    exp = G.msm([1] * n, pts)
+    S = gm_ctx.copy_to_device(sb)
+    P = gm_ctx.copy_points_to_device(cname, pb, g2)
+    _, aff = gm_ctx.msm(cname, S, P, n, g2)
+    assert pyref.decode_point(c, aff, g2) == exp
+    pre = gm_ctx.points_upload_precomputed(cname, pb, g2, 0)
+    _, aff = gm_ctx.msm_precomputed(cname, S, pre, n, g2)
+    assert pyref.decode_point(c, aff, g2) == exp
+    for b in (S, P, pre):
+        b.free()
