@@ -132,6 +132,7 @@ struct gm_g16_pk {
   size_t n, nb_wires, nb_public, nbA, nbB, nbK;
   void *A, *B, *Z, *K, *B2;       // device point arrays
   void *idxA, *idxB, *idxK;       // device index maps (compaction)
+  size_t zlo = 0, nbZ = 0;        // this shard's slice of h / pk.G1.Z (whole: 0, n-1)
   bool precomp = false;           // GM_PK_PRECOMPUTE: fixed-base window copies
   MsmPrecomp preA, preB, preZ, preK;  // layouts (B and B2 share preB)
   std::vector<uint8_t> alpha, beta, delta, beta2, delta2;  // host affine
@@ -627,12 +628,28 @@ int gm_g16_pk_upload(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, gm_g16_pk*
 }
 
 int gm_g16_pk_upload_ex(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsigned flags, gm_g16_pk** out) {
+  return gm_g16_pk_upload_shard(ctx, curve, h, flags, 0, 1, out);
+}
+
+// [lo, hi) of rank's contiguous shard of n items (gnark_mi355x.shard_range)
+static void shard_of(size_t n, int rank, int world, size_t* lo, size_t* hi) {
+  const size_t q = n / (size_t)world, r = n % (size_t)world;
+  *lo = (size_t)rank * q + std::min((size_t)rank, r);
+  *hi = *lo + q + ((size_t)rank < r ? 1 : 0);
+}
+
+int gm_g16_pk_upload_shard(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsigned flags, int rank, int world,
+                           gm_g16_pk** out) {
   if (int rc = check_curve(curve)) return rc;
   if (flags & ~(unsigned)GM_PK_PRECOMPUTE) {
     set_error("pk upload: unknown flags");
     return GM_ERR_INVALID;
   }
   if (!h || !out || h->domain_size < 2) return GM_ERR_INVALID;
+  if (world < 1 || rank < 0 || rank >= world) {
+    set_error("pk upload: bad rank / world");
+    return GM_ERR_INVALID;
+  }
   std::lock_guard<std::recursive_mutex> g(ctx->mu);
   GM_HIP(hipSetDevice(ctx->device));
   auto* pk = new gm_g16_pk();
@@ -640,15 +657,22 @@ int gm_g16_pk_upload_ex(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsigne
   pk->n = h->domain_size;
   pk->nb_wires = h->nb_wires;
   pk->nb_public = h->nb_public;
-  pk->nbA = h->nbA;
-  pk->nbB = h->nbB;
-  pk->nbK = h->nbK;
+  size_t loA, hiA, loB, hiB, loK, hiK, loZ, hiZ;
+  shard_of(h->nbA, rank, world, &loA, &hiA);
+  shard_of(h->nbB, rank, world, &loB, &hiB);
+  shard_of(h->nbK, rank, world, &loK, &hiK);
+  shard_of(pk->n - 1, rank, world, &loZ, &hiZ);
+  pk->nbA = hiA - loA;
+  pk->nbB = hiB - loB;
+  pk->nbK = hiK - loK;
+  pk->zlo = loZ;
+  pk->nbZ = hiZ - loZ;
   pk->precomp = (flags & GM_PK_PRECOMPUTE) != 0;
   const int frbits = curve == GM_BN254 ? CurveBN254::FR_BITS : CurveBLS12377::FR_BITS;
   if (pk->precomp) {
     pk->preA = msm_choose_precomp(pk->nbA, frbits);
     pk->preB = msm_choose_precomp(pk->nbB, frbits);
-    pk->preZ = msm_choose_precomp(pk->n - 1, frbits);
+    pk->preZ = msm_choose_precomp(pk->nbZ, frbits);
     pk->preK = msm_choose_precomp(pk->nbK, frbits);
   }
   const size_t g1b = 2 * fp_bytes(curve), g2b = 4 * fp_bytes(curve);
@@ -703,39 +727,41 @@ int gm_g16_pk_upload_ex(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsigne
     hipFree(tmp);
     return r;
   };
+  auto fail = [&](int code) {
+    for (void* q : {pk->A, pk->B, pk->Z, pk->K, pk->B2, pk->idxA, pk->idxB, pk->idxK})
+      if (q) hipFree(q);
+    delete pk;
+    return code;
+  };
+  // point arrays: the caller passes this shard's slice (first point = index lo)
   if ((rc = up_pts(h->g1_A, pk->nbA, false, pk->preA, &pk->A)) ||
       (rc = up_pts(h->g1_B, pk->nbB, false, pk->preB, &pk->B)) ||
-      (rc = up_pts(h->g1_Z, pk->n - 1, false, pk->preZ, &pk->Z)) ||
+      (rc = up_pts(h->g1_Z, pk->nbZ, false, pk->preZ, &pk->Z)) ||
       (rc = up_pts(h->g1_K, pk->nbK, false, pk->preK, &pk->K)) ||
-      (rc = up_pts(h->g2_B, pk->nbB, true, pk->preB, &pk->B2))) {
-    delete pk;
-    return rc;
-  }
+      (rc = up_pts(h->g2_B, pk->nbB, true, pk->preB, &pk->B2)))
+    return fail(rc);
   // compaction maps (prove.go:157-178: drop wire i when InfinityA[i] / InfinityB[i])
   std::vector<uint32_t> ia, ib, ik;
   for (size_t i = 0; i < pk->nb_wires; i++) {
     if (!h->infA[i]) ia.push_back((uint32_t)i);
     if (!h->infB[i]) ib.push_back((uint32_t)i);
   }
-  for (size_t i = 0; i < pk->nbK; i++) {
+  for (size_t i = 0; i < h->nbK; i++) {
     const size_t w = h->k_wires ? (size_t)h->k_wires[i] : pk->nb_public + i;
     if (w >= pk->nb_wires || w < pk->nb_public) {
       set_error("pk upload: K wire index out of range");
-      delete pk;
-      return GM_ERR_INVALID;
+      return fail(GM_ERR_INVALID);
     }
     ik.push_back((uint32_t)w);
   }
-  if (ia.size() != pk->nbA || ib.size() != pk->nbB || pk->nb_public + pk->nbK > pk->nb_wires) {
+  if (ia.size() != h->nbA || ib.size() != h->nbB || pk->nb_public + h->nbK > pk->nb_wires) {
     set_error("pk upload: infinity masks inconsistent with nbA/nbB/nbK");
-    delete pk;
-    return GM_ERR_INVALID;
+    return fail(GM_ERR_INVALID);
   }
-  if ((rc = up(ia.data(), 4 * ia.size(), &pk->idxA)) || (rc = up(ib.data(), 4 * ib.size(), &pk->idxB)) ||
-      (rc = up(ik.data(), 4 * ik.size(), &pk->idxK))) {
-    delete pk;
-    return rc;
-  }
+  // this shard's slices of the compaction maps
+  if ((rc = up(ia.data() + loA, 4 * pk->nbA, &pk->idxA)) || (rc = up(ib.data() + loB, 4 * pk->nbB, &pk->idxB)) ||
+      (rc = up(ik.data() + loK, 4 * pk->nbK, &pk->idxK)))
+    return fail(rc);
   auto cp = [](std::vector<uint8_t>& v, const void* s, size_t b) {
     v.resize(b);
     memcpy(v.data(), s, b);
@@ -856,7 +882,7 @@ static int g16_prove_t(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, void* 
   // Krs = MSM(wK, K) + kr delta + MSM(h[:n-1], Z) + s Ar + r Bs1   (computeKRS icicle.go:326-375)
   if ((rc = msm_device<C, false>(ctx, wK.p, pk->K, pk->nbK, t1, true, pK))) return rc;
   J1 krs = host::jadd(J1{t1[0], t1[1], t1[2]}, d2);
-  if ((rc = msm_device<C, false>(ctx, a, pk->Z, n - 1, t1, true, pZ))) return rc;
+  if ((rc = msm_device<C, false>(ctx, (char*)a + 32 * pk->zlo, pk->Z, pk->nbZ, t1, true, pZ))) return rc;
   krs = host::jadd(krs, J1{t1[0], t1[1], t1[2]});
   cross.join();
   krs = host::jadd(krs, s_ar);
@@ -911,4 +937,138 @@ int gm_g16_prove(gm_ctx* ctx, gm_g16_pk* pk, const void* wires, const void* a, c
   return gm_g16_prove_device(ctx, pk, w.p, da.p, db.p, dc.p, nc, r, s, ar_out, bs_out, krs_out);
 }
 
+// ---- sharded Groth16 (BASELINE config 4) -------------------------------
+int gm_g16_partial_bytes(int curve, size_t* out) {
+  if (int rc = check_curve(curve)) return rc;
+  if (out) *out = 4 * 3 * fp_bytes(curve) + 3 * 2 * fp_bytes(curve);
+  return GM_OK;
+}
+}  // extern "C"
+
+extern "C++" {
+// The five raw MSM sums of this shard: computeH (whole domain), then the A, B,
+// K, Z (h slice) G1 MSMs and the B G2 MSM over the shard's slices.
+template <class C>
+static int g16_partial_t(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, void* a, void* b, void* c, size_t nc,
+                         uint8_t* out) {
+  using HF1 = typename C::HG1F;
+  using HF2 = typename C::HG2F;
+  hipStream_t st = ctx->stream;
+  int rc;
+  Arena arena(ctx);
+  DevBuf wA, wB, wK;
+  if ((rc = wA.alloc(arena, 32 * (pk->nbA ? pk->nbA : 1))) || (rc = wB.alloc(arena, 32 * (pk->nbB ? pk->nbB : 1))) ||
+      (rc = wK.alloc(arena, 32 * (pk->nbK ? pk->nbK : 1))))
+    return rc;
+  {
+    ProfScope ps(ctx, "gather_scalars");
+    if (pk->nbA)
+      hipLaunchKernelGGL(k_gather_fr, dim3(blocks_for(pk->nbA, 256)), dim3(256), 0, st, (const uint4*)wires_dev,
+                         (const uint32_t*)pk->idxA, pk->nbA, (uint4*)wA.p);
+    if (pk->nbB)
+      hipLaunchKernelGGL(k_gather_fr, dim3(blocks_for(pk->nbB, 256)), dim3(256), 0, st, (const uint4*)wires_dev,
+                         (const uint32_t*)pk->idxB, pk->nbB, (uint4*)wB.p);
+    if (pk->nbK)
+      hipLaunchKernelGGL(k_gather_fr, dim3(blocks_for(pk->nbK, 256)), dim3(256), 0, st, (const uint4*)wires_dev,
+                         (const uint32_t*)pk->idxK, pk->nbK, (uint4*)wK.p);
+  }
+  GM_HIP(hipGetLastError());
+  if ((rc = compute_h_device<C>(ctx, a, b, c, nc, pk->n))) return rc;
+  const MsmPrecomp* pA = pk->precomp ? &pk->preA : nullptr;
+  const MsmPrecomp* pB = pk->precomp ? &pk->preB : nullptr;
+  const MsmPrecomp* pK = pk->precomp ? &pk->preK : nullptr;
+  const MsmPrecomp* pZ = pk->precomp ? &pk->preZ : nullptr;
+  HF1 t[3];
+  constexpr size_t J1 = sizeof(t);
+  if ((rc = msm_device<C, false>(ctx, wA.p, pk->A, pk->nbA, t, true, pA))) return rc;
+  memcpy(out, t, J1);
+  HF2 t2[3];
+  {
+    Arena parena(ctx);
+    MsmPlan planB;
+    if ((rc = msm_plan<C>(ctx, parena, wB.p, pk->nbB, pB, planB))) return rc;
+    if ((rc = msm_run<C, false>(ctx, planB, pk->B, t))) return rc;
+    memcpy(out + J1, t, J1);
+    if ((rc = msm_run<C, true>(ctx, planB, pk->B2, t2))) return rc;
+    memcpy(out + 4 * J1, t2, sizeof(t2));
+  }
+  if ((rc = msm_device<C, false>(ctx, wK.p, pk->K, pk->nbK, t, true, pK))) return rc;
+  memcpy(out + 2 * J1, t, J1);
+  if ((rc = msm_device<C, false>(ctx, (char*)a + 32 * pk->zlo, pk->Z, pk->nbZ, t, true, pZ))) return rc;
+  memcpy(out + 3 * J1, t, J1);
+  return GM_OK;
+}
+
+// Proof elements from the summed MSMs (icicle.go:295-391 / prove.go:195-305):
+//   Ar  = sum_A + alpha + [r]delta
+//   Bs1 = sum_B + beta + [s]delta
+//   Krs = sum_K + [-rs]delta + sum_Z + [s]Ar + [r]Bs1
+//   Bs  = sum_B2 + [s]delta2 + beta2
+template <class C>
+static int g16_finish_t(const gm_g16_pk_host* h, const uint8_t* sums, const void* r_mont, const void* s_mont,
+                        void* ar_out, void* bs_out, void* krs_out) {
+  using HF1 = typename C::HG1F;
+  using HF2 = typename C::HG2F;
+  using HFr = typename C::HFr;
+  using J1 = host::Jac<HF1>;
+  using J2 = host::Jac<HF2>;
+  host::F<HFr> r, s;
+  memcpy(r.v, r_mont, 32);
+  memcpy(s.v, s_mont, 32);
+  host::F<HFr> kr = -(r * s);
+  host::F<HFr> rc_ = host::from_mont(r), sc_ = host::from_mont(s), krc = host::from_mont(kr);
+  host::Aff<HF1> alpha, beta, delta;
+  host::Aff<HF2> beta2, delta2;
+  memcpy(&alpha, h->g1_alpha, sizeof(alpha));
+  memcpy(&beta, h->g1_beta, sizeof(beta));
+  memcpy(&delta, h->g1_delta, sizeof(delta));
+  memcpy(&beta2, h->g2_beta, sizeof(beta2));
+  memcpy(&delta2, h->g2_delta, sizeof(delta2));
+  J1 sum[4];
+  J2 sum2;
+  for (int k = 0; k < 4; k++) memcpy(&sum[k], sums + k * sizeof(J1), sizeof(J1));
+  memcpy(&sum2, sums + 4 * sizeof(J1), sizeof(J2));
+  const J1 dj = host::to_jac(delta);
+  J1 ar = host::jadd(host::jadd_aff(sum[0], alpha), host::jmul(dj, rc_.v, 4));
+  J1 bs1 = host::jadd(host::jadd_aff(sum[1], beta), host::jmul(dj, sc_.v, 4));
+  J1 krs = host::jadd(sum[2], host::jmul(dj, krc.v, 4));
+  krs = host::jadd(krs, sum[3]);
+  krs = host::jadd(krs, host::jmul(ar, sc_.v, 4));
+  krs = host::jadd(krs, host::jmul(bs1, rc_.v, 4));
+  J2 bs = host::jadd(sum2, host::jmul(host::to_jac(delta2), sc_.v, 4));
+  bs = host::jadd_aff(bs, beta2);
+  host::Aff<HF1> ara = host::to_aff(ar), krsa = host::to_aff(krs);
+  host::Aff<HF2> bsa = host::to_aff(bs);
+  memcpy(ar_out, &ara, sizeof(ara));
+  memcpy(krs_out, &krsa, sizeof(krsa));
+  memcpy(bs_out, &bsa, sizeof(bsa));
+  return GM_OK;
+}
+}  // extern "C++"
+
+extern "C" {
+int gm_g16_prove_partial(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, void* a_dev, void* b_dev, void* c_dev,
+                         size_t nc, void* partial_out) {
+  if (!ctx || !pk || !partial_out) return GM_ERR_INVALID;
+  if (nc > pk->n) {
+    set_error("prove: more constraints than the domain size");
+    return GM_ERR_INVALID;
+  }
+  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  GM_HIP(hipSetDevice(ctx->device));
+  int rc = pk->curve == GM_BN254
+               ? g16_partial_t<CurveBN254>(ctx, pk, wires_dev, a_dev, b_dev, c_dev, nc, (uint8_t*)partial_out)
+               : g16_partial_t<CurveBLS12377>(ctx, pk, wires_dev, a_dev, b_dev, c_dev, nc, (uint8_t*)partial_out);
+  prof_collect(ctx);
+  return rc;
+}
+
+int gm_g16_finish(int curve, const gm_g16_pk_host* h, const void* sums, const void* r, const void* s, void* ar_out,
+                  void* bs_out, void* krs_out) {
+  if (int rc = check_curve(curve)) return rc;
+  if (!h || !sums || !r || !s || !ar_out || !bs_out || !krs_out) return GM_ERR_INVALID;
+  return curve == GM_BN254
+             ? g16_finish_t<CurveBN254>(h, (const uint8_t*)sums, r, s, ar_out, bs_out, krs_out)
+             : g16_finish_t<CurveBLS12377>(h, (const uint8_t*)sums, r, s, ar_out, bs_out, krs_out);
+}
 }  // extern "C"

@@ -1,6 +1,10 @@
 // Radix sort of the MSM digit keys (bucket index) with their point-index
 // payloads -- the one non-templated piece of the MSM pipeline, kept in its own
 // translation unit (rocPRIM's sort is heavy to compile).
+//
+// (Measured on MI355X at 2^20 BN254 / 16.7M pairs with 20-bit keys: the
+// library default 0.43 ms; forced 8-bit warp-match places 0.59 ms; 11-bit
+// places, two passes, 1.88 ms -- the default stays.)
 #include <hipcub/hipcub.hpp>
 
 #include "msm.hpp"

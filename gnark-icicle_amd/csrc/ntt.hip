@@ -48,6 +48,10 @@ GM_DEV uint32_t brev_bits(uint32_t x, int bits) { return bits ? (__brev(x) >> (3
 //   pre     first pass only: multiply on load (coset powers)
 //   post    last pass only: multiply on store (1/n, coset^-1, 1/(g^n - 1))
 //
+// Butterflies are Harvey-style lazy: tile values live in [0, 2p) between stages
+// (no final subtraction in the twiddle product, 2p offsets instead of sign
+// tests; field.hpp "Lazily reduced arithmetic"), canonical again on store.
+//
 // Butterfly enumeration of a stage with half-size m = 2^lm (NBF = 512 per tile):
 //  * m <= 2: twiddle-index-major, so each wave shares one twiddle index jj and the
 //    jj == 0 butterflies (twiddle 1: all of stage m = 1, half of m = 2) skip their
@@ -120,9 +124,16 @@ __global__ void __launch_bounds__(NTT_TPB) k_ntt_pass(Fe<P>* __restrict__ data, 
         bfly_index(q, lm, lgB, jj, ol, grp);
         const int j0 = (grp << (lm + 1)) + jj, j1 = j0 + m;
         const Fe<P> u = X[j0 * B + ol], v = X[j1 * B + ol];
-        X[j0 * B + ol] = fe_add(u, v);
-        const Fe<P> d = fe_sub(u, v);
-        X[j1 * B + ol] = jj ? fe_mul(d, SW[jj * step]) : d;
+        Fe<P> s = fe_add_lz(u, v);                    // < 4p
+        fe_reduce_k<2>(s);
+        X[j0 * B + ol] = s;
+        Fe<P> d = fe_sub_lz<2>(u, v);                 // < 4p
+        if (jj) {
+          d = fe_mul_lz(d, SW[jj * step]);            // 4p * p < R' p: < 2p
+        } else {
+          fe_reduce_k<2>(d);
+        }
+        X[j1 * B + ol] = d;
       }
       __syncthreads();
     }
@@ -135,9 +146,12 @@ __global__ void __launch_bounds__(NTT_TPB) k_ntt_pass(Fe<P>* __restrict__ data, 
         const int j0 = (grp << (lm + 1)) + jj, j1 = j0 + m;
         const Fe<P> u = X[j0 * B + ol];
         Fe<P> v = X[j1 * B + ol];
-        if (jj) v = fe_mul(v, SW[jj * step]);
-        X[j0 * B + ol] = fe_add(u, v);
-        X[j1 * B + ol] = fe_sub(u, v);
+        if (jj) v = fe_mul_lz(v, SW[jj * step]);      // < 2p
+        Fe<P> s = fe_add_lz(u, v), d = fe_sub_lz<2>(u, v);  // both < 4p
+        fe_reduce_k<2>(s);
+        fe_reduce_k<2>(d);
+        X[j0 * B + ol] = s;
+        X[j1 * B + ol] = d;
       }
       __syncthreads();
     }
@@ -156,9 +170,10 @@ __global__ void __launch_bounds__(NTT_TPB) k_ntt_pass(Fe<P>* __restrict__ data, 
     if (o >= nother) continue;
     const size_t hi = o >> lo, L = o & lomask;
     const size_t addr = (hi << (lo + t)) + ((size_t)j << lo) + L;
-    Fe<P> v = X[j * B + ol];
+    Fe<P> v = X[j * B + ol];  // < 2p (lazy butterflies); canonical before the store
     if (!DIT && lo > 0) v = fe_mul(v, ld_tab(tw, ((size_t)j << lo) + L));
     if (post) v = fe_mul(v, ld_tab(post, addr));
+    if (!(!DIT && lo > 0) && !post) fe_reduce_once(v);
     st_fe(data, addr, v);
   }
 }

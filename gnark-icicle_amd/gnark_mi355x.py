@@ -42,7 +42,8 @@ SYMBOLS = [
     "gm_set_msm_window", "gm_malloc", "gm_free", "gm_copy_to_device", "gm_memcpy_h2d",
     "gm_memcpy_d2h", "gm_memcpy_d2d", "gm_copy_points_to_device", "gm_msm", "gm_msm_host_scalars", "gm_points_upload", "gm_msm_prepared", "gm_precompute_layout", "gm_points_upload_precomputed",
     "gm_msm_precomputed", "gm_kzg_commit", "gm_ntt",
-    "gm_poly_ops", "gm_reverse_scalars", "gm_groth16_compute_h", "gm_g16_pk_upload", "gm_g16_pk_upload_ex",
+    "gm_poly_ops", "gm_reverse_scalars", "gm_groth16_compute_h", "gm_g16_pk_upload", "gm_g16_pk_upload_ex", "gm_g16_pk_upload_shard",
+    "gm_g16_partial_bytes", "gm_g16_prove_partial", "gm_g16_finish",
     "gm_g16_pk_free", "gm_g16_prove", "gm_g16_prove_device", "gm_jac_add", "gm_jac_to_affine",
     "gm_batch_mul_base", "gm_random_scalars", "gm_generator", "gm_test_field_op",
     "gm_test_point_op",
@@ -96,6 +97,10 @@ def load_library(path: str = LIB_PATH):
     L.gm_groth16_compute_h.argtypes = [vp, i, vp, vp, vp, sz, sz]
     L.gm_g16_pk_upload.argtypes = [vp, i, vp, pvp]
     L.gm_g16_pk_upload_ex.argtypes = [vp, i, vp, ctypes.c_uint, pvp]
+    L.gm_g16_pk_upload_shard.argtypes = [vp, i, vp, ctypes.c_uint, i, i, pvp]
+    L.gm_g16_partial_bytes.argtypes = [i, ctypes.POINTER(sz)]
+    L.gm_g16_prove_partial.argtypes = [vp, vp, vp, vp, vp, vp, sz, vp]
+    L.gm_g16_finish.argtypes = [i, vp, vp, vp, vp, vp, vp, vp]
     L.gm_g16_pk_free.argtypes = [vp, vp]
     L.gm_g16_prove.argtypes = [vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, vp, vp]
     L.gm_g16_prove_device.argtypes = [vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, vp, vp]
@@ -460,6 +465,38 @@ class _PkHost(ctypes.Structure):
                                                 "g2_beta", "g2_delta", "g2_B", "infA", "infB", "k_wires"]]
 
 
+def _pk_host_struct(curve, pk: dict, domain_size: int, nb_wires: int, nb_public: int, shard=None,
+                    pk_is_shard: bool = False):
+    """gm_g16_pk_host for `pk` (a dict of gnark-layout arrays, see ProvingKey).
+    shard = (rank, world): point arrays are sliced to the rank's shard unless
+    pk_is_shard (they already are; the counts then come from pk['shard_sizes'])."""
+    g1b, g2b = point_bytes(curve, False), point_bytes(curve, True)
+    arrs = {k: _buf(v) for k, v in pk.items() if k not in ("sizes", "shard_sizes", "k_wires")}
+    h = _PkHost()
+    h.domain_size, h.nb_wires, h.nb_public = domain_size, nb_wires, nb_public
+    if pk_is_shard:
+        h.nbA, h.nbB, h.nbK = pk["shard_sizes"]
+    else:
+        h.nbA = arrs["g1_A"].size // g1b
+        h.nbB = arrs["g1_B"].size // g1b
+        h.nbK = arrs["g1_K"].size // g1b
+    if "k_wires" in pk and pk["k_wires"] is not None:
+        kw = np.ascontiguousarray(np.asarray(pk["k_wires"], dtype=np.uint32))
+        h.nbK = kw.size
+        h.k_wires = kw.ctypes.data
+        arrs["k_wires"] = kw
+    if shard is not None and not pk_is_shard:
+        rank, world = shard
+        for key, count, pb in (("g1_A", h.nbA, g1b), ("g1_B", h.nbB, g1b), ("g1_K", h.nbK, g1b),
+                               ("g1_Z", domain_size - 1, g1b), ("g2_B", h.nbB, g2b)):
+            lo, hi = shard_range(count, world, rank)
+            arrs[key] = arrs[key][pb * lo:pb * hi].copy() if hi > lo else np.zeros(pb, np.uint8)
+    for k in ["g1_alpha", "g1_beta", "g1_delta", "g1_A", "g1_B", "g1_Z", "g1_K", "g2_beta", "g2_delta",
+              "g2_B", "infA", "infB"]:
+        setattr(h, k, arrs[k].ctypes.data)
+    return h, arrs
+
+
 class ProvingKey:
     """Device-resident Groth16 proving key (icicle_bn254.ProvingKey + deviceInfo,
     provingkey.go:10-28; uploaded once like setupDevicePointers, icicle.go:31-130).
@@ -468,35 +505,30 @@ class ProvingKey:
     g1_B, g1_Z (n-1, bit-reversed), g1_K, g2_beta, g2_delta, g2_B, infA, infB, and
     optionally k_wires (the wire index of each pk.G1.K point when BSB22
     commitments filter K, prove.go:243-245; default nb_public + i).
+
+    shard = (rank, world) keeps only this rank's slice of every point array on
+    the device (gm_g16_pk_upload_shard; sharded_prove); with pk_is_shard the
+    point arrays in `pk` already are the slices and pk['shard_sizes'] = (nbA, nbB, nbK)
+    gives the whole key's counts.
     """
 
     PRECOMPUTE = 1  # GM_PK_PRECOMPUTE
 
     def __init__(self, ctx: Context, curve, pk: dict, domain_size: int, nb_wires: int, nb_public: int,
-                 precompute: bool = False):
+                 precompute: bool = False, shard=None, pk_is_shard: bool = False):
         self.ctx = ctx
         self.curve = curve_id(curve)
-        g1b = point_bytes(curve, False)
-        arrs = {k: _buf(v) for k, v in pk.items() if k not in ("sizes", "k_wires")}
-        h = _PkHost()
-        h.domain_size, h.nb_wires, h.nb_public = domain_size, nb_wires, nb_public
-        h.nbA = arrs["g1_A"].size // g1b
-        h.nbB = arrs["g1_B"].size // g1b
-        h.nbK = arrs["g1_K"].size // g1b
-        for k in ["g1_alpha", "g1_beta", "g1_delta", "g1_A", "g1_B", "g1_Z", "g1_K", "g2_beta", "g2_delta",
-                  "g2_B", "infA", "infB"]:
-            setattr(h, k, arrs[k].ctypes.data)
-        if "k_wires" in pk and pk["k_wires"] is not None:
-            kw = np.ascontiguousarray(np.asarray(pk["k_wires"], dtype=np.uint32))
-            h.nbK = kw.size
-            h.k_wires = kw.ctypes.data
-            arrs["k_wires"] = kw
+        h, arrs = _pk_host_struct(curve, pk, domain_size, nb_wires, nb_public, shard, pk_is_shard)
         self._keep = arrs
+        self._h = h
         handle = ctypes.c_void_p()
-        _check(load_library().gm_g16_pk_upload_ex(ctx.handle, self.curve, ctypes.byref(h),
-                                                  self.PRECOMPUTE if precompute else 0, ctypes.byref(handle)))
+        flags = self.PRECOMPUTE if precompute else 0
+        rank, world = shard if shard is not None else (0, 1)
+        _check(load_library().gm_g16_pk_upload_shard(ctx.handle, self.curve, ctypes.byref(h), flags, rank, world,
+                                                     ctypes.byref(handle)))
         self.handle = handle
         self.n, self.nb_wires, self.nb_public = domain_size, nb_wires, nb_public
+        self.shard = (rank, world)
 
     def free(self):
         if self.handle:
@@ -522,3 +554,51 @@ class ProvingKey:
         _check(load_library().gm_g16_prove_device(self.ctx.handle, self.handle, wires.ptr, a.ptr, b.ptr, c.ptr,
                                                   nb_constraints, _p(R), _p(S), _p(ar), _p(bs), _p(krs)))
         return ar.tobytes(), bs.tobytes(), krs.tobytes()
+
+    def prove_partial_device(self, wires: DeviceBuffer, a: DeviceBuffer, b: DeviceBuffer, c: DeviceBuffer,
+                             nb_constraints: int) -> bytes:
+        """This shard's raw MSM sums (gm_g16_prove_partial): 4 G1Jac + 1 G2Jac."""
+        out = np.zeros(g16_partial_bytes(self.curve), np.uint8)
+        _check(load_library().gm_g16_prove_partial(self.ctx.handle, self.handle, wires.ptr, a.ptr, b.ptr, c.ptr,
+                                                   nb_constraints, _p(out)))
+        return out.tobytes()
+
+
+def g16_partial_bytes(curve) -> int:
+    n = ctypes.c_size_t()
+    _check(load_library().gm_g16_partial_bytes(curve_id(curve), ctypes.byref(n)))
+    return n.value
+
+
+def g16_reduce_partials(curve, partials) -> bytes:
+    """Component-wise host sum of rank partials [A, B, K, Z (G1Jac), B2 (G2Jac)]."""
+    j1, j2 = jac_bytes(curve, False), jac_bytes(curve, True)
+    out = []
+    for k in range(5):
+        g2 = k == 4
+        lo = 4 * j1 if g2 else k * j1
+        sz = j2 if g2 else j1
+        out.append(reduce_partials(curve, g2, [bytes(p)[lo:lo + sz] for p in partials]))
+    return b"".join(out)
+
+
+def g16_finish(curve, pk_host: "_PkHost", sums: bytes, r: bytes, s: bytes):
+    """(Ar, Bs, Krs) affine bytes from summed partials (gm_g16_finish, host only)."""
+    S, R, SS = _buf(sums), _buf(r), _buf(s)
+    ar = np.zeros(point_bytes(curve, False), np.uint8)
+    krs = np.zeros(point_bytes(curve, False), np.uint8)
+    bs = np.zeros(point_bytes(curve, True), np.uint8)
+    _check(load_library().gm_g16_finish(curve_id(curve), ctypes.byref(pk_host), _p(S), _p(R), _p(SS), _p(ar),
+                                        _p(bs), _p(krs)))
+    return ar.tobytes(), bs.tobytes(), krs.tobytes()
+
+
+def sharded_prove(pk: ProvingKey, wires: DeviceBuffer, a: DeviceBuffer, b: DeviceBuffer, c: DeviceBuffer,
+                  nb_constraints: int, r: bytes, s: bytes, group=None, device=None):
+    """Multi-GPU Groth16 prove (BASELINE config 4): every rank computes its
+    shard's five MSM sums, the fixed-size partials are all-gathered (RCCL over
+    xGMI for backend "nccl", gloo on CPU) and every rank sums them and applies
+    the blinding on the host.  Returns (Ar, Bs, Krs) on every rank."""
+    local = pk.prove_partial_device(wires, a, b, c, nb_constraints)
+    parts = allgather_partial(local, group=group, device=device)
+    return g16_finish(pk.curve, pk._h, g16_reduce_partials(pk.curve, parts), r, s)

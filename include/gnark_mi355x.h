@@ -192,6 +192,30 @@ int gm_g16_prove_device(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, void*
                         void* b_dev, void* c_dev, size_t nb_constraints, const void* r,
                         const void* s, void* ar_out, void* bs_out, void* krs_out);
 
+/* ---- sharded Groth16 (BASELINE config 4: G1/G2 MSMs split across the GPUs of
+ *      a node, one process per GPU) -------------------------
+ * Rank `rank` of `world` uploads only its contiguous slice [lo, hi) of each
+ * point array (lo/hi as gnark_mi355x.shard_range: the first n % world ranks
+ * hold one extra point) of pk.G1.A (nbA), pk.G1.B and pk.G2.B (nbB), pk.G1.K
+ * (nbK) and pk.G1.Z (n - 1).  In `pk` the counts nbA/nbB/nbK and the flags
+ * infA/infB/k_wires describe the WHOLE key, while g1_A, g1_B, g1_K, g1_Z and
+ * g2_B point at the first point of this rank's slice.  world = 1 is
+ * gm_g16_pk_upload_ex. */
+int gm_g16_pk_upload_shard(gm_ctx* ctx, int curve, const gm_g16_pk_host* pk, unsigned flags, int rank,
+                           int world, gm_g16_pk** out);
+/* Size of one partial: 4 G1Jac (sums over A, B, K, Z) + 1 G2Jac (B2). */
+int gm_g16_partial_bytes(int curve, size_t* out);
+/* computeH over the whole domain (every rank holds the solved a, b, c and the
+ * wires), then the five MSMs over this rank's slices: writes the raw sums
+ * [sum_A, sum_B, sum_K, sum_Z] (G1Jac) and sum_B2 (G2Jac), no blinding. */
+int gm_g16_prove_partial(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, void* a_dev, void* b_dev,
+                         void* c_dev, size_t nb_constraints, void* partial_out);
+/* Host only: proof elements from the rank-summed partials (same layout) with
+ * the blinding of icicle.go:295-391 (alpha, beta, [r]delta, [s]delta,
+ * [-rs]delta, [s]Ar, [r]Bs1, [s]delta2, beta2 from `pk`). */
+int gm_g16_finish(int curve, const gm_g16_pk_host* pk, const void* sums, const void* r, const void* s,
+                  void* ar_out, void* bs_out, void* krs_out);
+
 /* ---- host-side group helpers (finishing adds of sharded MSMs) ---------- */
 /* out = p + q, all gnark Jacobian (G1Jac or G2Jac). */
 int gm_jac_add(int curve, int g2, const void* p, const void* q, void* out);

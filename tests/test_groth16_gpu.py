@@ -109,3 +109,45 @@ def test_groth16_k_wire_filter(gm_ctx, oracle):
     finally:
         dpk.free()
     assert got == exp
+
+
+@pytest.mark.parametrize("cname,k,world,precompute", [("bn254", 1023, 2, False), ("bn254", 4000, 3, True),
+                                                      ("bls12377", 511, 2, False), ("bn254", 15, 4, False)])
+def test_groth16_sharded_partials(gm_ctx, oracle, cname, k, world, precompute):
+    """BASELINE config 4 data path on one GPU: every rank's pk shard
+    (gm_g16_pk_upload_shard) and partial MSM sums (gm_g16_prove_partial) are
+    computed in turn, summed and finished on the host (gm_g16_finish): the proof
+    must be byte-identical to the CPU restatement.  world=4 at n=16 leaves
+    ragged and tiny shards."""
+    import gnark_mi355x as gm
+    c = pyref.CURVES[cname]
+    r1, W = R.squaring_chain(k, cname, x=5)
+    tox = R.encode_vec(cname, [t % c.r for t in TOXIC])
+    pk = oracle.g16_setup(cname, r1, tox)
+    a, b, cc = r1.solve_abc(W)
+    enc = lambda v: R.encode_vec(cname, v)
+    rb, sb = enc([0x5151]), enc([0x7373])
+    exp = oracle.g16_prove(cname, pk, r1.nb_public, enc(W), enc(a), enc(b), enc(cc), rb, sb)
+    n = r1.domain_size
+    parts = []
+    for rank in range(world):
+        dpk = gm.ProvingKey(gm_ctx, cname, pk, n, r1.nb_wires, r1.nb_public, precompute=precompute,
+                            shard=(rank, world))
+        bufs = []
+        try:
+            Wd = gm_ctx.copy_to_device(enc(W))
+            bufs.append(Wd)
+            abc = []
+            for v in (a, b, cc):
+                d = gm_ctx.malloc(32 * n)
+                d.write(bytes(32 * n))
+                d.write(enc(v))
+                abc.append(d)
+            bufs += abc
+            parts.append(dpk.prove_partial_device(Wd, *abc, len(a)))
+        finally:
+            for x in bufs:
+                x.free()
+            dpk.free()
+    got = gm.g16_finish(cname, dpk._h, gm.g16_reduce_partials(cname, parts), rb, sb)
+    assert got == exp
