@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--msm-extra", type=int, default=1, help="secondary G2 / BLS12-377 MSM lines (0 = skip)")
     ap.add_argument("--g16-plain", type=str, default="20",
                     help="Groth16 domains also proved with a plain (non-precomputed) pk")
+    ap.add_argument("--g16-sharded-logn", type=int, default=24,
+                    help="N>1: sharded Groth16 prove domain (BASELINE config 4; 0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
     return ap.parse_args()
@@ -71,8 +73,11 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
+        # one process per GPU; GM_BENCH_BACKEND=gloo (and a device index modulo the
+        # visible GPUs) only to rehearse the N>1 code path on a one-GPU box
+        local_rank = local_rank % max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+        dist.init_process_group(os.environ.get("GM_BENCH_BACKEND", "nccl"))
     import gnark_mi355x as gm
 
     ctx = gm.Context(local_rank)
@@ -92,7 +97,7 @@ def main():
 
     def step():
         if dist is not None:
-            return gm.sharded_msm(ctx, "bn254", S, P, n, device="cuda")
+            return gm.sharded_msm(ctx, "bn254", S, P, n)
         return ctx.msm("bn254", S, P, n)[0]
 
     for _ in range(args.warmup):
@@ -108,7 +113,7 @@ def main():
     ctx.profile(False)
     stats = ctx.profile_stats()
     if dist is not None:
-        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([dt], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     ms_per_step = dt * 1e3 / args.steps
@@ -164,6 +169,10 @@ def main():
 
     if rank == 0 and not args.no_secondary and world == 1:
         out["secondary"] = secondary(ctx, gm, args)
+    if world > 1 and not args.no_secondary and args.g16_sharded_logn:
+        g = groth16_sharded_bench(ctx, gm, args.g16_sharded_logn, rank, world, dist, torch)
+        if rank == 0:
+            out["secondary"] = {"groth16_sharded": g}
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(S, P, n, res)
     if rank == 0:
@@ -284,6 +293,75 @@ def groth16_bench(ctx, gm, logn, precompute=True):
         b.free()
     return {"logn": logn, "prove_ms": round(min(times) * 1e3, 3), "pk": "precomputed" if precompute else "plain",
             "note": "inputs device-resident; after Solve"}
+
+
+def groth16_sharded_bench(ctx, gm, logn, rank, world, dist, torch):
+    """BASELINE config 4: Groth16 prove at n = 2^logn with the G1/G2 MSMs sharded
+    across the ranks (one GPU each).  Every rank holds only its slice of each pk
+    point array (synthetic random points, precomputed) and the replicated solved
+    vectors; computeH runs on every rank, the five partial MSM sums are
+    all-gathered over RCCL and finished on the host (gnark_mi355x.sharded_prove).
+    Timed with barriers + device syncs on both sides, max over ranks."""
+    n = 1 << logn
+    nb_wires = n + 2
+    nb_public = 2
+    gen1, gen2 = gm.generator("bn254", False), gm.generator("bn254", True)
+
+    def pts(count, g2, seed):
+        import numpy as np
+        if count == 0:
+            return np.zeros(0, np.uint8)
+        k = ctx.random_scalars("bn254", count, seed)
+        p = ctx.batch_mul_base("bn254", g2, gen2 if g2 else gen1, k, count)
+        b = p.to_host()
+        k.free()
+        p.free()
+        return np.frombuffer(b, np.uint8)
+
+    import numpy as np
+    one1 = pts(3, False, 1)
+    one2 = pts(2, True, 2)
+    nbA = nbB = nb_wires
+    nbK = nb_wires - nb_public
+
+    def sl(count):
+        lo, hi = gm.shard_range(count, world, rank)
+        return hi - lo
+
+    sd = 1000 * (rank + 1)
+    pk = {"g1_alpha": one1[:64], "g1_beta": one1[64:128], "g1_delta": one1[128:192],
+          "g1_A": pts(sl(nbA), False, sd + 3), "g1_B": pts(sl(nbB), False, sd + 4),
+          "g1_Z": pts(sl(n - 1), False, sd + 5), "g1_K": pts(sl(nbK), False, sd + 6),
+          "g2_beta": one2[:128], "g2_delta": one2[128:256], "g2_B": pts(sl(nbB), True, sd + 7),
+          "infA": np.zeros(nb_wires, np.uint8), "infB": np.zeros(nb_wires, np.uint8),
+          "shard_sizes": (nbA, nbB, nbK)}
+    dpk = gm.ProvingKey(ctx, "bn254", pk, n, nb_wires, nb_public, precompute=True, shard=(rank, world),
+                        pk_is_shard=True)
+    W = ctx.random_scalars("bn254", nb_wires, 8)
+    A, B, C = (ctx.malloc(32 * n) for _ in range(3))
+    srcs = [ctx.random_scalars("bn254", n, 9 + i) for i in range(3)]
+    r = ctx.random_scalars("bn254", 2, 12).to_host()
+    times = []
+    for _ in range(2):
+        for dst, src in zip((A, B, C), srcs):
+            dst.copy_from(src)
+        ctx.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        gm.sharded_prove(dpk, W, A, B, C, n, r[:32], r[32:])
+        ctx.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        tt = torch.tensor([dt], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        times.append(float(tt.item()))
+    dpk.free()
+    for b in [W, A, B, C] + srcs:
+        b.free()
+    return {"logn": logn, "n_gpus": world, "prove_ms": round(min(times) * 1e3, 3), "pk": "precomputed, sharded",
+            "note": "computeH replicated per rank; 5 MSMs sharded; partials all-gathered over RCCL; after Solve"}
 
 
 def cpu_baseline(S, P, n, gpu_jac):
