@@ -145,6 +145,49 @@ GM_DEV void xyzz_add_aff_lz(XYZZ<Fe<P>>& a, const Affine<Fe<P>>& p) {
   a.y = fe_sub_lz<2>(fe_mul_lz(R, fe_sub_lz<8>(Q, X3)), fe_mul_lz(a.y, PPP));  // R (<6p) * (<10p); < 4p
   a.x = X3;
 }
+// Lazily reduced a += p for G2 buckets (Fp2 coordinates).  Invariants: every
+// component of a.x, a.y, a.zz, a.zzz < 2p; p canonical.  Product inputs stay
+// below 4p per component (see fe2_mul_lz / fe2_sqr_lz).
+template <class P, int BETA>
+GM_DEV void xyzz_add_aff_lz(XYZZ<Fe2<P, BETA>>& a, const Affine<Fe2<P, BETA>>& p) {
+  static_assert(P::BITS + 7 <= RADIX * P::N, "lazy reduction needs R' > 128 p");
+  using F = Fe2<P, BETA>;
+  if (aff_is_inf(p)) return;
+  if (xyzz_is_inf(a)) {
+    a.x = p.x;
+    a.y = p.y;
+    a.zz = FOps<F>::one();
+    a.zzz = FOps<F>::one();
+    return;
+  }
+  F Pd = fe2_sub_lz<2>(fe2_mul_lz(p.x, a.zz), a.x);   // U2 - X1   < 4p
+  F R = fe2_sub_lz<2>(fe2_mul_lz(p.y, a.zzz), a.y);   // S2 - Y1   < 4p
+  if (fe_is_zero_lz<4>(Pd.a0) && fe_is_zero_lz<4>(Pd.a1)) {
+    if (fe_is_zero_lz<4>(R.a0) && fe_is_zero_lz<4>(R.a1)) {
+      a = xyzz_dbl_aff(p);
+    } else {
+      a = xyzz_inf<F>();
+    }
+    return;
+  }
+  F PP = fe2_sqr_lz<4>(Pd);                            // < 2p
+  F PPP = fe2_mul_lz(Pd, PP);                          // < 2p
+  a.zz = fe2_mul_lz(a.zz, PP);
+  F Q = fe2_mul_lz(a.x, PP);                           // < 2p
+  a.zzz = fe2_mul_lz(a.zzz, PPP);
+  F X3 = fe2_sub_lz<4>(fe2_sub_lz<2>(fe2_sqr_lz<4>(R), PPP), fe2_add_lz(Q, Q));  // < 8p
+  fe2_to2p<8>(X3);
+  F Y3 = fe2_sub_lz<2>(fe2_mul_lz(R, fe2_sub_lz<2>(Q, X3)), fe2_mul_lz(a.y, PPP));  // < 4p
+  fe2_to2p<4>(Y3);
+  a.x = X3;
+  a.y = Y3;
+}
+template <class P, int BETA>
+GM_DEV XYZZ<Fe2<P, BETA>> xyzz_canon_lz(const XYZZ<Fe2<P, BETA>>& a) {
+  auto c = [](const Fe2<P, BETA>& v) { return Fe2<P, BETA>{fe_canon<1>(v.a0), fe_canon<1>(v.a1)}; };
+  return {c(a.x), c(a.y), c(a.zz), c(a.zzz)};
+}
+
 // canonical form of a lazily accumulated bucket
 template <class P>
 GM_DEV XYZZ<Fe<P>> xyzz_canon_lz(const XYZZ<Fe<P>>& a) {

@@ -533,6 +533,79 @@ GM_DEV Fe2<P, BETA> fe_inv(const Fe2<P, BETA>& a) {
   return {fe_mul(a.a0, ni), fe_neg(fe_mul(a.a1, ni))};
 }
 
+// ---- lazily reduced Fp2 (G2 bucket accumulation) ---------------------------
+// Components are normalised back below 2p after every product, so product
+// inputs stay small: with components < IN p (IN <= 6 in the G2 mixed add) the
+// Karatsuba term (a0 + a1)(b0 + b1) < 144 p^2 < R' p for BN254 (R' / p > 169);
+// BLS12-377 Fp has R' / p ~ 2^29.
+// x < M p  ->  x < 2p  (M <= 16)
+template <int M, class P>
+GM_DEV void fe_to2p(Fe<P>& x) {
+  static_assert(M <= 16, "fe_to2p covers x < 16p");
+  if constexpr (M > 8) fe_reduce_k<8>(x);
+  if constexpr (M > 4) fe_reduce_k<4>(x);
+  if constexpr (M > 2) fe_reduce_k<2>(x);
+}
+template <class P, int BETA>
+GM_DEV Fe2<P, BETA> fe2_add_lz(const Fe2<P, BETA>& a, const Fe2<P, BETA>& b) {
+  return {fe_add_lz(a.a0, b.a0), fe_add_lz(a.a1, b.a1)};
+}
+template <int K, class P, int BETA>
+GM_DEV Fe2<P, BETA> fe2_sub_lz(const Fe2<P, BETA>& a, const Fe2<P, BETA>& b) {
+  return {fe_sub_lz<K>(a.a0, b.a0), fe_sub_lz<K>(a.a1, b.a1)};
+}
+template <int M, class P, int BETA>
+GM_DEV void fe2_to2p(Fe2<P, BETA>& x) {
+  fe_to2p<M>(x.a0);
+  fe_to2p<M>(x.a1);
+}
+// 5 x for x < 2p (< 10p)
+template <class P>
+GM_DEV Fe<P> fe_times5_lz(const Fe<P>& x) {
+  const Fe<P> x2 = fe_add_lz(x, x);
+  return fe_add_lz(fe_add_lz(x2, x2), x);
+}
+// Karatsuba product, result components < 2p.  Inputs: components < 6p (BN254).
+template <class P, int BETA>
+GM_DEV Fe2<P, BETA> fe2_mul_lz(const Fe2<P, BETA>& a, const Fe2<P, BETA>& b) {
+  const Fe<P> v0 = fe_mul_lz(a.a0, b.a0);  // < 2p
+  const Fe<P> v1 = fe_mul_lz(a.a1, b.a1);  // < 2p
+  const Fe<P> s = fe_mul_lz(fe_add_lz(a.a0, a.a1), fe_add_lz(b.a0, b.a1));  // < 2p
+  Fe2<P, BETA> r;
+  if constexpr (BETA == -1) {
+    r.a0 = fe_sub_lz<2>(v0, v1);  // < 4p
+    fe_to2p<4>(r.a0);
+  } else {
+    static_assert(BETA == -5, "unsupported non-residue");
+    r.a0 = fe_sub_lz<10>(v0, fe_times5_lz(v1));  // < 12p
+    fe_to2p<12>(r.a0);
+  }
+  r.a1 = fe_sub_lz<4>(s, fe_add_lz(v0, v1));  // < 6p
+  fe_to2p<6>(r.a1);
+  return r;
+}
+// Complex squaring, result components < 2p.  Inputs: components < IN p.
+template <int IN, class P, int BETA>
+GM_DEV Fe2<P, BETA> fe2_sqr_lz(const Fe2<P, BETA>& a) {
+  const Fe<P> c = fe_mul_lz(a.a0, a.a1);  // < 2p
+  Fe2<P, BETA> r;
+  if constexpr (BETA == -1) {
+    // (a0 + a1)(a0 - a1): (2 IN p)^2 <= 144 p^2 for IN <= 6
+    r.a0 = fe_mul_lz(fe_add_lz(a.a0, a.a1), fe_sub_lz<IN>(a.a0, a.a1));
+  } else {
+    static_assert(BETA == -5, "unsupported non-residue");
+    // (a0 + a1)(a0 - 5 a1) + 4 a0 a1
+    const Fe<P> a15 = fe_times5_lz(a.a1);  // < 5 IN p
+    const Fe<P> t = fe_mul_lz(fe_add_lz(a.a0, a.a1), fe_sub_lz<5 * IN>(a.a0, a15));
+    const Fe<P> c2 = fe_add_lz(c, c);
+    r.a0 = fe_add_lz(t, fe_add_lz(c2, c2));  // < 10p
+    fe_to2p<10>(r.a0);
+  }
+  r.a1 = fe_add_lz(c, c);  // < 4p
+  fe_to2p<4>(r.a1);
+  return r;
+}
+
 // gnark-layout <-> internal for a coordinate field (Fe or Fe2).
 template <class F>
 struct Coord;

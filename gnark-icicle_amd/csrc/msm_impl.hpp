@@ -158,7 +158,7 @@ GM_DEV PackedPt<PW> load_packed_pt(const uint32_t* __restrict__ src) {
 // edges go to part_first[t] / part_last[t] and are merged by k_msm_fixup.
 // Skewed scalar distributions (one huge bucket) therefore cost the same as
 // uniform ones in this phase.
-// G1 buckets accumulate lazily reduced (xyzz_add_aff_lz); G2 canonically.
+// Buckets accumulate lazily reduced (xyzz_add_aff_lz), canonical on emit.
 template <class F>
 struct LazyAcc {
   static constexpr bool on = false;
@@ -170,6 +170,12 @@ struct LazyAcc<Fe<P>> {
   static constexpr bool on = true;
   GM_DEV static void add(XYZZ<Fe<P>>& a, const Affine<Fe<P>>& p) { xyzz_add_aff_lz(a, p); }
   GM_DEV static XYZZ<Fe<P>> canon(const XYZZ<Fe<P>>& a) { return xyzz_canon_lz(a); }
+};
+template <class P, int B>
+struct LazyAcc<Fe2<P, B>> {
+  static constexpr bool on = true;
+  GM_DEV static void add(XYZZ<Fe2<P, B>>& a, const Affine<Fe2<P, B>>& p) { xyzz_add_aff_lz(a, p); }
+  GM_DEV static XYZZ<Fe2<P, B>> canon(const XYZZ<Fe2<P, B>>& a) { return xyzz_canon_lz(a); }
 };
 
 template <class F>
