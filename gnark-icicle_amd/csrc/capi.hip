@@ -155,6 +155,7 @@ int gm_init(int device, gm_ctx** out) {
   auto* c = new gm_ctx();
   c->device = device;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking);
   if (e != hipSuccess) {
     set_error(std::string("hipStreamCreate: ") + hipGetErrorString(e));
     delete c;
@@ -168,6 +169,7 @@ int gm_destroy(gm_ctx* ctx) {
   if (!ctx) return GM_OK;
   hipSetDevice(ctx->device);
   hipStreamSynchronize(ctx->stream);
+  if (ctx->aux) hipStreamSynchronize(ctx->aux);
   ntt_domains_free(ctx);
   for (auto& ch : ctx->chunks) hipFree(ch.base);
   ctx->chunks.clear();
@@ -177,6 +179,7 @@ int gm_destroy(gm_ctx* ctx) {
     hipEventDestroy(p.b);
   }
   hipStreamDestroy(ctx->stream);
+  if (ctx->aux) hipStreamDestroy(ctx->aux);
   delete ctx;
   return GM_OK;
 }
@@ -786,6 +789,42 @@ int gm_g16_pk_free(gm_ctx* ctx, gm_g16_pk* pk) {
 }
 
 extern "C++" {
+// computeH on the context's auxiliary stream, after everything already queued
+// on the main stream (the caller's a, b, c uploads).  The NTT passes overlap the
+// A, B and K MSMs, whose sorts, reductions and host round trips leave the VALUs
+// idle; wait() makes the main stream wait for h before the Z MSM.  The
+// destructor drains the auxiliary stream on every exit path.
+struct AuxComputeH {
+  gm_ctx* ctx;
+  hipEvent_t ev_in = nullptr, ev_h = nullptr;
+  explicit AuxComputeH(gm_ctx* c) : ctx(c) {}
+  template <class C>
+  int start(void* a, void* b, void* c, size_t nc, size_t n) {
+    GM_HIP(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
+    GM_HIP(hipEventCreateWithFlags(&ev_h, hipEventDisableTiming));
+    GM_HIP(hipEventRecord(ev_in, ctx->stream));
+    GM_HIP(hipStreamWaitEvent(ctx->aux, ev_in, 0));
+    hipStream_t main = ctx->stream;
+    ctx->stream = ctx->aux;
+    int rc = compute_h_device<C>(ctx, a, b, c, nc, n);
+    ctx->stream = main;
+    if (rc) return rc;
+    GM_HIP(hipEventRecord(ev_h, ctx->aux));
+    return GM_OK;
+  }
+  int wait() {
+    GM_HIP(hipStreamWaitEvent(ctx->stream, ev_h, 0));
+    return GM_OK;
+  }
+  ~AuxComputeH() {
+    hipStreamSynchronize(ctx->aux);
+    if (ev_in) hipEventDestroy(ev_in);
+    if (ev_h) hipEventDestroy(ev_h);
+  }
+};
+}  // extern "C++"
+
+extern "C++" {
 template <class C>
 static int g16_prove_t(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, void* a, void* b,
                        void* c, size_t nc, const void* r_mont, const void* s_mont, void* ar_out,
@@ -846,8 +885,10 @@ static int g16_prove_t(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, void* 
       if (t.joinable()) t.join();
     }
   } joiner{deltas};
-  // H (computeH, icicle.go:453-513 / prove.go:356-399) -> bit-reversed h in `a`
-  if ((rc = compute_h_device<C>(ctx, a, b, c, nc, n))) return rc;
+  // H (computeH, icicle.go:453-513 / prove.go:356-399) -> bit-reversed h in `a`,
+  // on the auxiliary stream, overlapped with the A, B and K MSMs
+  AuxComputeH hjob(ctx);
+  if ((rc = hjob.start<C>(a, b, c, nc, n))) return rc;
   HF1 t1[3];
   const MsmPrecomp* pA = pk->precomp ? &pk->preA : nullptr;
   const MsmPrecomp* pB = pk->precomp ? &pk->preB : nullptr;
@@ -882,6 +923,7 @@ static int g16_prove_t(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, void* 
   // Krs = MSM(wK, K) + kr delta + MSM(h[:n-1], Z) + s Ar + r Bs1   (computeKRS icicle.go:326-375)
   if ((rc = msm_device<C, false>(ctx, wK.p, pk->K, pk->nbK, t1, true, pK))) return rc;
   J1 krs = host::jadd(J1{t1[0], t1[1], t1[2]}, d2);
+  if ((rc = hjob.wait())) return rc;
   if ((rc = msm_device<C, false>(ctx, (char*)a + 32 * pk->zlo, pk->Z, pk->nbZ, t1, true, pZ))) return rc;
   krs = host::jadd(krs, J1{t1[0], t1[1], t1[2]});
   cross.join();
@@ -973,7 +1015,8 @@ static int g16_partial_t(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, void
                          (const uint32_t*)pk->idxK, pk->nbK, (uint4*)wK.p);
   }
   GM_HIP(hipGetLastError());
-  if ((rc = compute_h_device<C>(ctx, a, b, c, nc, pk->n))) return rc;
+  AuxComputeH hjob(ctx);
+  if ((rc = hjob.start<C>(a, b, c, nc, pk->n))) return rc;
   const MsmPrecomp* pA = pk->precomp ? &pk->preA : nullptr;
   const MsmPrecomp* pB = pk->precomp ? &pk->preB : nullptr;
   const MsmPrecomp* pK = pk->precomp ? &pk->preK : nullptr;
@@ -994,6 +1037,7 @@ static int g16_partial_t(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, void
   }
   if ((rc = msm_device<C, false>(ctx, wK.p, pk->K, pk->nbK, t, true, pK))) return rc;
   memcpy(out + 2 * J1, t, J1);
+  if ((rc = hjob.wait())) return rc;
   if ((rc = msm_device<C, false>(ctx, (char*)a + 32 * pk->zlo, pk->Z, pk->nbZ, t, true, pZ))) return rc;
   memcpy(out + 3 * J1, t, J1);
   return GM_OK;

@@ -35,6 +35,7 @@ struct KernelStat {
 struct gm_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t aux = nullptr;  // second stream: work overlapped with `stream` inside one call
   std::recursive_mutex mu;
   // per-kernel profiling with HIP events on this context's stream
   bool profiling = false;
