@@ -180,6 +180,7 @@ int gm_destroy(gm_ctx* ctx) {
   }
   hipStreamDestroy(ctx->stream);
   if (ctx->aux) hipStreamDestroy(ctx->aux);
+  if (ctx->pinned) hipHostFree(ctx->pinned);
   delete ctx;
   return GM_OK;
 }

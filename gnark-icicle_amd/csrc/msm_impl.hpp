@@ -22,6 +22,7 @@
 #include "msm.hpp"
 #include "runtime.hpp"
 
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 
@@ -570,10 +571,10 @@ int msm_run(gm_ctx* ctx, const MsmPlan& plan, const void* points_internal,
   if ((rc = wsum.alloc(arena, sizeof(uint32_t) * 4 * WORDS * Wr * (2 + c)))) return rc;
   const uint32_t* pts_internal = reinterpret_cast<const uint32_t*>(points_internal);
   const uint32_t* offsets = plan.offsets;
+  DevBuf pfirst, plast;
   {
     const uint32_t K = ctx->msm_slice ? (uint32_t)ctx->msm_slice : 64u;
     const size_t nslices = (M + K - 1) / K;
-    DevBuf pfirst, plast;
     if ((rc = pfirst.alloc(arena, sizeof(XYZZ<DF>) * nslices))) return rc;
     if ((rc = plast.alloc(arena, sizeof(XYZZ<DF>) * nslices))) return rc;
     GM_HIP(hipMemsetAsync(buckets.p, 0, sizeof(XYZZ<DF>) * (size_t)total, st));  // all-zero XYZZ = infinity
@@ -590,26 +591,22 @@ int msm_run(gm_ctx* ctx, const MsmPlan& plan, const void* points_internal,
     hipLaunchKernelGGL(k_msm_fixup<DF>, dim3(blocks_for(total, 128)), dim3(128), 0, st, offsets, total, K,
                        buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>(),
                        errw.as<uint32_t>() + 1);
-    uint32_t maxspan = 0;
-    GM_HIP(hipMemcpyAsync(&maxspan, errw.as<uint32_t>() + 1, 4, hipMemcpyDeviceToHost, st));
-    GM_HIP(hipStreamSynchronize(st));
-    if (maxspan > FIX_SERIAL) {
-      for (uint32_t d = 0; (1u << d) < maxspan; d++)
-        hipLaunchKernelGGL(k_msm_fix_tree<DF>, dim3(blocks_for(nslices, 128)), dim3(128), 0, st, plan.keys,
-                           offsets, total, K, (uint32_t)nslices, d, pfirst.as<XYZZ<DF>>());
-      hipLaunchKernelGGL(k_msm_fixup_long<DF>, dim3(blocks_for(total, 128)), dim3(128), 0, st, offsets, total,
-                         K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>());
-    }
   }
+  // Bucket reduction, launched speculatively: buckets spanning more than
+  // FIX_SERIAL slices (skewed scalars) are only known once errw[1] (max span)
+  // reaches the host, so the reduction is queued right away and redone after the
+  // long-span fixup in that (rare) case -- one host round trip per MSM instead of two.
   uint32_t Q = 2;  // points per node: [G, U, Y_0..Y_{Q-3}]
-  {
+  XYZZ<DF>* cur = nullptr;
+  auto reduce = [&]() -> int {
     ProfScope ps(ctx, "msm_bucket_reduce");
+    Q = 2;
     hipLaunchKernelGGL(k_msm_seg<DF>, dim3(blocks_for((size_t)Wr * nseg, 128)), dim3(128), 0, st,
                        buckets.as<XYZZ<DF>>(), nb, L, nseg, Wr, nodes_a.as<XYZZ<DF>>());
     // LDS tree levels until one node per window
     constexpr size_t SLOT_BUDGET = (96u << 10) / sizeof(XYZZ<DF>);
     uint32_t m = nseg;
-    XYZZ<DF>* cur = nodes_a.as<XYZZ<DF>>();
+    cur = nodes_a.as<XYZZ<DF>>();
     XYZZ<DF>* nxt = nodes_b.as<XYZZ<DF>>();
     while (m > 1) {
       uint32_t lg = 0;
@@ -629,18 +626,69 @@ int msm_run(gm_ctx* ctx, const MsmPlan& plan, const void* points_internal,
     }
     hipLaunchKernelGGL(k_msm_export<DF>, dim3(blocks_for((size_t)Wr * Q, 128)), dim3(128), 0, st, cur, Wr * Q,
                        wsum.as<uint32_t>());
-  }
-  GM_HIP(hipGetLastError());
-  uint32_t herr = 0;
-  GM_HIP(hipMemcpyAsync(&herr, errw.p, 4, hipMemcpyDeviceToHost, st));
-  std::vector<HF> hw(4 * (size_t)Wr * Q);
+    GM_HIP(hipGetLastError());
+    return GM_OK;
+  };
   static_assert(sizeof(HF) == 4 * WORDS, "host/device layout mismatch");
-  GM_HIP(hipMemcpyAsync(hw.data(), wsum.p, sizeof(uint32_t) * 4 * WORDS * Wr * Q, hipMemcpyDeviceToHost, st));
-  GM_HIP(hipStreamSynchronize(st));
+  uint8_t* stage = nullptr;
+  auto readback = [&]() -> int {
+    const size_t wbytes = sizeof(uint32_t) * 4 * WORDS * Wr * Q;
+    void* pb;
+    if (int r = pinned_buf(ctx, 16 + wbytes, &pb)) return r;
+    stage = reinterpret_cast<uint8_t*>(pb);
+    GM_HIP(hipMemcpyAsync(stage, errw.p, 16, hipMemcpyDeviceToHost, st));
+    GM_HIP(hipMemcpyAsync(stage + 16, wsum.p, wbytes, hipMemcpyDeviceToHost, st));
+    GM_HIP(hipStreamSynchronize(st));
+    return GM_OK;
+  };
+  // Speculate only when uniform scalars would give no long span: the fullest
+  // bucket is then a top-window digit (n / 2^top_bits entries; plus the other
+  // windows' share when buckets are shared).  Large MSMs whose top window is
+  // narrow (2^24: 1024-4096 entries per top digit) sync on max span first.
+  {
+    const uint32_t K = ctx->msm_slice ? (uint32_t)ctx->msm_slice : 64u;
+    const int top_bits = C::FR_BITS - (int)(c * (plan.W - 1));
+    double fullest = (double)plan.n / std::ldexp(1.0, top_bits > 0 ? top_bits : 0);
+    if (Wr == 1 && plan.W > 1) fullest += (double)(plan.W - 1) * (double)plan.n / (double)nb;
+    if (fullest > 0.5 * FIX_SERIAL * K) {
+      void* pb;
+      if ((rc = pinned_buf(ctx, 16, &pb))) return rc;
+      GM_HIP(hipMemcpyAsync(pb, errw.p, 16, hipMemcpyDeviceToHost, st));
+      GM_HIP(hipStreamSynchronize(st));
+      uint32_t ms;
+      memcpy(&ms, (uint8_t*)pb + 4, 4);
+      if (ms > FIX_SERIAL) {
+        const size_t nslices = (M + K - 1) / K;
+        for (uint32_t d = 0; (1u << d) < ms; d++)
+          hipLaunchKernelGGL(k_msm_fix_tree<DF>, dim3(blocks_for(nslices, 128)), dim3(128), 0, st, plan.keys,
+                             offsets, total, K, (uint32_t)nslices, d, pfirst.as<XYZZ<DF>>());
+        hipLaunchKernelGGL(k_msm_fixup_long<DF>, dim3(blocks_for(total, 128)), dim3(128), 0, st, offsets, total,
+                           K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>());
+        GM_HIP(hipMemsetAsync(errw.as<uint32_t>() + 1, 0, 4, st));  // long spans resolved
+      }
+    }
+  }
+  if ((rc = reduce()) || (rc = readback())) return rc;
+  uint32_t herr, maxspan;
+  memcpy(&herr, stage, 4);
+  memcpy(&maxspan, stage + 4, 4);
+  if (maxspan > FIX_SERIAL) {
+    const uint32_t K = ctx->msm_slice ? (uint32_t)ctx->msm_slice : 64u;
+    const size_t nslices = (M + K - 1) / K;
+    for (uint32_t d = 0; (1u << d) < maxspan; d++)
+      hipLaunchKernelGGL(k_msm_fix_tree<DF>, dim3(blocks_for(nslices, 128)), dim3(128), 0, st, plan.keys, offsets,
+                         total, K, (uint32_t)nslices, d, pfirst.as<XYZZ<DF>>());
+    hipLaunchKernelGGL(k_msm_fixup_long<DF>, dim3(blocks_for(total, 128)), dim3(128), 0, st, offsets, total, K,
+                       buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>());
+    if ((rc = reduce()) || (rc = readback())) return rc;
+    memcpy(&herr, stage, 4);
+  }
   if (herr) {
     set_error("msm: internal consistency check failed (code " + std::to_string(herr) + ")");
     return GM_ERR_DEVICE;
   }
+  std::vector<HF> hw(4 * (size_t)Wr * Q);
+  memcpy(hw.data(), stage + 16, sizeof(HF) * hw.size());
   // Host Horner over bit positions: window w contributes U_w at 2^(c w) and
   // Y_{w,b} at 2^(c w + log2 L + b) (b < Q - 2 = log2(nseg), so every exponent
   // stays below c (w + 1)).  Shared buckets: one window, w = 0.

@@ -36,6 +36,9 @@ struct gm_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipStream_t aux = nullptr;  // second stream: work overlapped with `stream` inside one call
+  // pinned host staging for small device->host readbacks (truly async copies)
+  void* pinned = nullptr;
+  size_t pinned_cap = 0;
   std::recursive_mutex mu;
   // per-kernel profiling with HIP events on this context's stream
   bool profiling = false;
@@ -154,6 +157,24 @@ struct Arena {
     return GM_OK;
   }
 };
+
+// Pinned host staging of at least `bytes` (grown on demand; freed by gm_destroy).
+inline int pinned_buf(gm_ctx* ctx, size_t bytes, void** out) {
+  if (ctx->pinned_cap < bytes) {
+    if (ctx->pinned) hipHostFree(ctx->pinned);
+    ctx->pinned = nullptr;
+    ctx->pinned_cap = 0;
+    size_t cap = bytes < (size_t(256) << 10) ? (size_t(256) << 10) : bytes;
+    hipError_t e = hipHostMalloc(&ctx->pinned, cap, hipHostMallocDefault);
+    if (e != hipSuccess) {
+      set_error(std::string("hipHostMalloc: ") + hipGetErrorString(e));
+      return GM_ERR_OOM;
+    }
+    ctx->pinned_cap = cap;
+  }
+  *out = ctx->pinned;
+  return GM_OK;
+}
 
 // A typed view of one arena allocation.
 struct DevBuf {
