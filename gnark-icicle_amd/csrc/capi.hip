@@ -3,6 +3,7 @@
 // (backend/groth16/bn254/icicle/icicle.go:133-422), re-derived from the current
 // CPU prover groth16_bn254.Prove (backend/groth16/bn254/prove.go:62-325) as
 // SURVEY.md §0.3 prescribes: only the MSMs and NTTs move to the device.
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 #include <string>
@@ -801,6 +802,9 @@ struct AuxComputeH {
   explicit AuxComputeH(gm_ctx* c) : ctx(c) {}
   template <class C>
   int start(void* a, void* b, void* c, size_t nc, size_t n) {
+    // GM_G16_OVERLAP=0: computeH in order on the main stream (A/B measurements)
+    static const bool overlap = !getenv("GM_G16_OVERLAP") || atoi(getenv("GM_G16_OVERLAP")) != 0;
+    if (!overlap) return compute_h_device<C>(ctx, a, b, c, nc, n);
     GM_HIP(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
     GM_HIP(hipEventCreateWithFlags(&ev_h, hipEventDisableTiming));
     GM_HIP(hipEventRecord(ev_in, ctx->stream));
@@ -814,7 +818,7 @@ struct AuxComputeH {
     return GM_OK;
   }
   int wait() {
-    GM_HIP(hipStreamWaitEvent(ctx->stream, ev_h, 0));
+    if (ev_h) GM_HIP(hipStreamWaitEvent(ctx->stream, ev_h, 0));
     return GM_OK;
   }
   ~AuxComputeH() {
