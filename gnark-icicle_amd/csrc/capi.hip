@@ -155,6 +155,8 @@ int gm_init(int device, gm_ctx** out) {
   GM_HIP(hipSetDevice(device));
   auto* c = new gm_ctx();
   c->device = device;
+  // GM_MSM_SLICE: entries per thread in the bucket accumulation (tuning; default 64)
+  if (const char* sl = getenv("GM_MSM_SLICE")) c->msm_slice = atoi(sl) > 0 ? atoi(sl) : 0;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking);
   if (e != hipSuccess) {
