@@ -33,6 +33,7 @@ MsmPrecomp msm_choose_precomp(size_t n, int bits);
 struct MsmPlan {
   uint32_t c = 0, W = 0, nb = 0, total = 0;
   uint32_t Wred = 0;  // windows reduced separately: W (plain) or 1 (shared buckets)
+  uint32_t dW = 0;    // digit-major keys with dW windows (KeyFmt, msm_impl.hpp), 0 = window-major
   size_t n = 0, M = 0;
   size_t npts = 0;    // points addressable through the plan (bounds check)
   uint32_t* keys = nullptr;     // sorted bucket keys, M entries

@@ -44,6 +44,24 @@ GM_DEV uint32_t window_bits(const FeG<Fr>& k, uint32_t bit, uint32_t mask) {
   return (uint32_t)(v >> sh) & mask;
 }
 
+// Decoding of the sorted (key, value) entries.  Window-major plans keep the
+// global bucket index w*nb + |d|-1 in the key.  Digit-major plans (W <= 16,
+// n < 2^27, see msm_plan) sort by |d|-1 alone -- c bits instead of
+// c + log2(W), one radix pass fewer at c = 16 -- and carry the window in value
+// bits 27..30: the sort is stable and its input window-major, so equal digits
+// stay ordered by window and b = (|d|-1) * W + w is ascending, i.e. the entries
+// are grouped by bucket in digit-major bucket order.  slot() maps b back to the
+// window-major bucket storage the reduction reads.
+struct KeyFmt {
+  uint32_t W = 0;  // 0: window-major keys; else digit-major with W windows
+  uint32_t nb = 0;
+  GM_HD uint32_t key(uint32_t k, uint32_t v) const {
+    return W ? (k >= nb ? W * nb : k * W + ((v >> 27) & 15u)) : k;
+  }
+  GM_HD uint32_t idx(uint32_t v) const { return v & (W ? 0x07ffffffu : 0x7fffffffu); }
+  GM_HD uint32_t slot(uint32_t b) const { return W ? (b % W) * nb + b / W : b; }
+};
+
 // gnark Montgomery fr.Element -> canonical integer as packed u32 words
 template <class Fr>
 GM_DEV FeG<Fr> load_scalar_canonical(const uint32_t* __restrict__ s, uint32_t i) {
@@ -58,7 +76,8 @@ GM_DEV FeG<Fr> load_scalar_canonical(const uint32_t* __restrict__ s, uint32_t i)
 template <class Fr>
 __global__ void __launch_bounds__(256) k_msm_keys(const uint32_t* __restrict__ scalars, uint32_t n,
                                                   uint32_t c, uint32_t W, uint32_t shared_stride,
-                                                  uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+                                                  uint32_t dmajor, uint32_t* __restrict__ keys,
+                                                  uint32_t* __restrict__ vals) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const FeG<Fr> k = load_scalar_canonical<Fr>(scalars, i);
@@ -80,6 +99,9 @@ __global__ void __launch_bounds__(256) k_msm_keys(const uint32_t* __restrict__ s
     if (shared_stride) {
       keys[e] = d ? d - 1 : nb;
       vals[e] = (w * shared_stride + i) | (neg << 31);
+    } else if (dmajor) {
+      keys[e] = d ? d - 1 : nb;
+      vals[e] = i | (w << 27) | (neg << 31);
     } else {
       keys[e] = d ? w * nb + d - 1 : total;
       vals[e] = i | (neg << 31);
@@ -183,11 +205,11 @@ template <class F>
 GM_DEV void accum_emit(uint32_t b, const XYZZ<F>& acc_raw, bool is_first, bool is_last, uint32_t start,
                        uint32_t end, uint32_t t, const uint32_t* __restrict__ offsets,
                        XYZZ<F>* __restrict__ buckets, XYZZ<F>* __restrict__ part_first,
-                       XYZZ<F>* __restrict__ part_last) {
+                       XYZZ<F>* __restrict__ part_last, KeyFmt fmt) {
   const XYZZ<F> acc = LazyAcc<F>::canon(acc_raw);
   const uint32_t bs = offsets[b], be = offsets[b + 1];
   if (bs >= start && be <= end) {
-    buckets[b] = acc;
+    buckets[fmt.slot(b)] = acc;
   } else {
     if (is_first) part_first[t] = acc;
     if (is_last) part_last[t] = acc;
@@ -202,17 +224,17 @@ GM_DEV void accum_seg_body(const uint32_t* __restrict__ points, uint32_t n,
                                                        uint32_t K, XYZZ<F>* __restrict__ buckets,
                                                        XYZZ<F>* __restrict__ part_first,
                                                        XYZZ<F>* __restrict__ part_last,
-                                                       uint32_t* __restrict__ err) {
+                                                       uint32_t* __restrict__ err, KeyFmt fmt) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t Mv = offsets[total];  // valid (non-zero-digit) entries
   const uint32_t start = t * K;
   if (start >= Mv) return;
   const uint32_t end = min(start + K, Mv);
-  uint32_t cur = keys[start];
+  uint32_t v = vals[start];
+  uint32_t cur = fmt.key(keys[start], v);
   bool first = true;
   XYZZ<F> acc = xyzz_inf<F>();
-  uint32_t v = vals[start];
-  uint32_t idx = v & 0x7fffffffu;
+  uint32_t idx = fmt.idx(v);
   if (idx >= n) {
     atomicOr(err, 2u);
     return;
@@ -220,13 +242,13 @@ GM_DEV void accum_seg_body(const uint32_t* __restrict__ points, uint32_t n,
   constexpr int PW = 2 * Coord<F>::WORDS;  // u32 words per packed point
   PackedPt<PW> P = load_packed_pt<PW>(points + (size_t)idx * PW);
   for (uint32_t q = start; q < end; q++) {
-    const uint32_t k = keys[q];
+    const uint32_t k = fmt.key(keys[q], v);
     // prefetch the next point's words while this add runs
     uint32_t vn = 0;
     PackedPt<PW> Pn;
     if (PREFETCH && q + 1 < end) {
       vn = vals[q + 1];
-      const uint32_t in = vn & 0x7fffffffu;
+      const uint32_t in = fmt.idx(vn);
       if (in >= n) {
         atomicOr(err, 2u);
         return;
@@ -234,12 +256,12 @@ GM_DEV void accum_seg_body(const uint32_t* __restrict__ points, uint32_t n,
       Pn = load_packed_pt<PW>(points + (size_t)in * PW);
     }
     if (k != cur) {
-      accum_emit(cur, acc, first, false, start, end, t, offsets, buckets, part_first, part_last);
+      accum_emit(cur, acc, first, false, start, end, t, offsets, buckets, part_first, part_last, fmt);
       first = false;
       acc = xyzz_inf<F>();
       cur = k;
     }
-    if (!PREFETCH) P = load_packed_pt<PW>(points + (size_t)(v & 0x7fffffffu) * PW);
+    if (!PREFETCH) P = load_packed_pt<PW>(points + (size_t)fmt.idx(v) * PW);
     Affine<F> A = load_affine_packed<F>(P.w);
     if (v >> 31) A.y = fe_neg(A.y);
     LazyAcc<F>::add(acc, A);
@@ -248,13 +270,13 @@ GM_DEV void accum_seg_body(const uint32_t* __restrict__ points, uint32_t n,
       P = Pn;
     } else if (q + 1 < end) {
       v = vals[q + 1];
-      if ((v & 0x7fffffffu) >= n) {
+      if (fmt.idx(v) >= n) {
         atomicOr(err, 2u);
         return;
       }
     }
   }
-  accum_emit(cur, acc, first, true, start, end, t, offsets, buckets, part_first, part_last);
+  accum_emit(cur, acc, first, true, start, end, t, offsets, buckets, part_first, part_last, fmt);
 }
 
 
@@ -266,8 +288,9 @@ __global__ void __launch_bounds__(128) k_msm_accum_seg(const uint32_t* __restric
                                                        const uint32_t* __restrict__ offsets, uint32_t total,
                                                        uint32_t K, XYZZ<F>* __restrict__ buckets,
                                                        XYZZ<F>* __restrict__ part_first,
-                                                       XYZZ<F>* __restrict__ part_last, uint32_t* __restrict__ err) {
-  accum_seg_body<F, true>(points, n, keys, vals, offsets, total, K, buckets, part_first, part_last, err);
+                                                       XYZZ<F>* __restrict__ part_last, uint32_t* __restrict__ err,
+                                                       KeyFmt fmt) {
+  accum_seg_body<F, true>(points, n, keys, vals, offsets, total, K, buckets, part_first, part_last, err, fmt);
 }
 
 // G2 (Fp2 coordinates): a mixed add keeps ~330 registers live, i.e. one wave per
@@ -278,8 +301,8 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2)))
 k_msm_accum_seg_g2(const uint32_t* __restrict__ points, uint32_t n, const uint32_t* __restrict__ keys,
                    const uint32_t* __restrict__ vals, const uint32_t* __restrict__ offsets, uint32_t total,
                    uint32_t K, XYZZ<F>* __restrict__ buckets, XYZZ<F>* __restrict__ part_first,
-                   XYZZ<F>* __restrict__ part_last, uint32_t* __restrict__ err) {
-  accum_seg_body<F, false>(points, n, keys, vals, offsets, total, K, buckets, part_first, part_last, err);
+                   XYZZ<F>* __restrict__ part_last, uint32_t* __restrict__ err, KeyFmt fmt) {
+  accum_seg_body<F, false>(points, n, keys, vals, offsets, total, K, buckets, part_first, part_last, err, fmt);
 }
 
 // Merge the partial sums of buckets cut by slice edges.  Bucket b spans slices
@@ -295,7 +318,7 @@ __global__ void __launch_bounds__(128) k_msm_fixup(const uint32_t* __restrict__ 
                                                    uint32_t K, XYZZ<F>* __restrict__ buckets,
                                                    const XYZZ<F>* __restrict__ part_first,
                                                    const XYZZ<F>* __restrict__ part_last,
-                                                   uint32_t* __restrict__ maxspan) {
+                                                   uint32_t* __restrict__ maxspan, KeyFmt fmt) {
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= total) return;
   const uint32_t bs = offsets[b], be = offsets[b + 1];
@@ -308,18 +331,19 @@ __global__ void __launch_bounds__(128) k_msm_fixup(const uint32_t* __restrict__ 
   }
   XYZZ<F> acc = part_last[t0];
   for (uint32_t t = t0 + 1; t <= t1; t++) acc = xyzz_add(acc, part_first[t]);
-  buckets[b] = acc;
+  buckets[fmt.slot(b)] = acc;
 }
 
 // One level d of the pairwise tree over part_first[t0+1 .. t1] of every long span.
 template <class F>
 __global__ void __launch_bounds__(128) k_msm_fix_tree(const uint32_t* __restrict__ keys,
+                                                      const uint32_t* __restrict__ vals,
                                                       const uint32_t* __restrict__ offsets, uint32_t total,
                                                       uint32_t K, uint32_t nslices, uint32_t d,
-                                                      XYZZ<F>* __restrict__ part_first) {
+                                                      XYZZ<F>* __restrict__ part_first, KeyFmt fmt) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nslices || (size_t)t * K >= offsets[total]) return;
-  const uint32_t b = keys[(size_t)t * K];
+  const uint32_t b = fmt.W ? fmt.key(keys[(size_t)t * K], vals[(size_t)t * K]) : keys[(size_t)t * K];
   const uint32_t t0 = offsets[b] / K, t1 = (offsets[b + 1] - 1) / K;
   if (t1 - t0 <= FIX_SERIAL || t <= t0) return;
   const uint32_t rel = t - (t0 + 1), len = t1 - t0, step = 1u << d;
@@ -331,14 +355,14 @@ template <class F>
 __global__ void __launch_bounds__(128) k_msm_fixup_long(const uint32_t* __restrict__ offsets, uint32_t total,
                                                         uint32_t K, XYZZ<F>* __restrict__ buckets,
                                                         const XYZZ<F>* __restrict__ part_first,
-                                                        const XYZZ<F>* __restrict__ part_last) {
+                                                        const XYZZ<F>* __restrict__ part_last, KeyFmt fmt) {
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= total) return;
   const uint32_t bs = offsets[b], be = offsets[b + 1];
   if (be == bs) return;
   const uint32_t t0 = bs / K, t1 = (be - 1) / K;
   if (t1 - t0 <= FIX_SERIAL) return;
-  buckets[b] = xyzz_add(part_last[t0], part_first[t0 + 1]);
+  buckets[fmt.slot(b)] = xyzz_add(part_last[t0], part_first[t0 + 1]);
 }
 
 // ---------------------------------------------------------------------------
@@ -436,7 +460,8 @@ __global__ void __launch_bounds__(128) k_msm_export(const XYZZ<F>* __restrict__ 
   Coord<F>::store_gnark(o + 3 * Coord<F>::WORDS, r.zzz);
 }
 
-// offsets[b] = first sorted position with key >= b (lower bound), b in [0, total]
+// offsets[b] = first sorted position with key >= b (lower bound), b in [0, total]:
+// window-major keys, one binary search per bucket.
 static __global__ void __launch_bounds__(256) k_msm_lower_bound(const uint32_t* __restrict__ keys, uint32_t M,
                                                          uint32_t total, uint32_t* __restrict__ offsets) {
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
@@ -448,6 +473,20 @@ static __global__ void __launch_bounds__(256) k_msm_lower_bound(const uint32_t* 
     else hi = mid;
   }
   offsets[b] = lo;
+}
+
+// Digit-major keys (two loads per probe make the binary search ~2x slower): the
+// same offsets from one linear pass -- entry q (q <= M) owns the buckets b with
+// key(q-1) < b <= key(q) (key(-1) = -1, key(M) = total) -- usually one write;
+// empty buckets in a gap are written by the entry that ends it.
+static __global__ void __launch_bounds__(256) k_msm_bounds(const uint32_t* __restrict__ keys,
+                                                    const uint32_t* __restrict__ vals, uint32_t M, uint32_t total,
+                                                    uint32_t* __restrict__ offsets, KeyFmt fmt) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q > M) return;
+  const uint32_t hi = q == M ? total : min(fmt.W ? fmt.key(keys[q], vals[q]) : keys[q], total);
+  const uint32_t lo = q == 0 ? 0u : (fmt.W ? fmt.key(keys[q - 1], vals[q - 1]) : keys[q - 1]) + 1;
+  for (uint32_t b = lo; b <= hi; b++) offsets[b] = q;
 }
 
 // ---------------------------------------------------------------------------
@@ -500,6 +539,16 @@ int msm_plan(gm_ctx* ctx, Arena& arena, const void* scalars_dev, size_t n, const
   plan.Wred = shared ? 1 : W;
   plan.total = plan.Wred * plan.nb;
   plan.npts = shared ? (size_t)W * pre->stride : n;
+  // digit-major keys (KeyFmt) when they save a radix pass: c bits instead of
+  // bits(W * nb); needs the window in 4 value bits and the index in 27
+  {
+    int wm_bits = 1;
+    while ((1ull << wm_bits) <= plan.total) wm_bits++;
+    static const char* dm = getenv("GM_MSM_DMAJOR");  // 0 = off (A/B)
+    const bool allow = !dm || atoi(dm) != 0;
+    if (allow && !shared && W <= 16 && n < (size_t(1) << 27) && (c + 7) / 8 < (uint32_t)(wm_bits + 7) / 8)
+      plan.dW = W;
+  }
   const size_t M = (size_t)W * n;
   plan.M = M;
   if (M >= (size_t(1) << 31)) {
@@ -516,11 +565,15 @@ int msm_plan(gm_ctx* ctx, Arena& arena, const void* scalars_dev, size_t n, const
     ProfScope ps(ctx, "msm_keys");
     hipLaunchKernelGGL(k_msm_keys<typename C::Fr>, dim3(blocks_for(n, 256)), dim3(256), 0, st,
                        reinterpret_cast<const uint32_t*>(scalars_dev), (uint32_t)n, c, W,
-                       shared ? (uint32_t)pre->stride : 0u, keys_in.as<uint32_t>(), vals_in.as<uint32_t>());
+                       shared ? (uint32_t)pre->stride : 0u, plan.dW ? 1u : 0u, keys_in.as<uint32_t>(),
+                       vals_in.as<uint32_t>());
   }
   GM_HIP(hipGetLastError());
+  // sort key range: bucket indices + the zero-digit sentinel (total), or for
+  // digit-major keys |d|-1 + the sentinel nb
+  const uint64_t key_max = plan.dW ? plan.nb : plan.total;
   int end_bit = 1;
-  while ((1ull << end_bit) <= plan.total) end_bit++;
+  while ((1ull << end_bit) <= key_max) end_bit++;
   {
     ProfScope ps(ctx, "msm_sort");
     if ((rc = msm_sort_pairs(ctx, arena, keys_in.as<uint32_t>(), keys_out.as<uint32_t>(), vals_in.as<uint32_t>(),
@@ -529,8 +582,15 @@ int msm_plan(gm_ctx* ctx, Arena& arena, const void* scalars_dev, size_t n, const
   }
   {
     ProfScope ps(ctx, "msm_offsets");
-    hipLaunchKernelGGL(k_msm_lower_bound, dim3(blocks_for((size_t)plan.total + 1, 256)), dim3(256), 0, st,
-                       keys_out.as<uint32_t>(), (uint32_t)M, plan.total, offsets.as<uint32_t>());
+    KeyFmt fmt;
+    fmt.W = plan.dW;
+    fmt.nb = plan.nb;
+    if (fmt.W)
+      hipLaunchKernelGGL(k_msm_bounds, dim3(blocks_for(M + 1, 256)), dim3(256), 0, st, keys_out.as<uint32_t>(),
+                         vals_out.as<uint32_t>(), (uint32_t)M, plan.total, offsets.as<uint32_t>(), fmt);
+    else
+      hipLaunchKernelGGL(k_msm_lower_bound, dim3(blocks_for((size_t)plan.total + 1, 256)), dim3(256), 0, st,
+                         keys_out.as<uint32_t>(), (uint32_t)M, plan.total, offsets.as<uint32_t>());
   }
   GM_HIP(hipGetLastError());
   plan.keys = keys_out.as<uint32_t>();
@@ -571,6 +631,9 @@ int msm_run(gm_ctx* ctx, const MsmPlan& plan, const void* points_internal,
   if ((rc = wsum.alloc(arena, sizeof(uint32_t) * 4 * WORDS * Wr * (2 + c)))) return rc;
   const uint32_t* pts_internal = reinterpret_cast<const uint32_t*>(points_internal);
   const uint32_t* offsets = plan.offsets;
+  KeyFmt fmt;
+  fmt.W = plan.dW;
+  fmt.nb = nb;
   DevBuf pfirst, plast;
   {
     const uint32_t K = ctx->msm_slice ? (uint32_t)ctx->msm_slice : 64u;
@@ -587,10 +650,10 @@ int msm_run(gm_ctx* ctx, const MsmPlan& plan, const void* points_internal,
     auto accum = noprefetch ? k_msm_accum_seg_g2<DF> : k_msm_accum_seg<DF>;
     hipLaunchKernelGGL(accum, dim3(blocks_for(nslices, 128)), dim3(128), 0, st, pts_internal,
                        (uint32_t)plan.npts, plan.keys, plan.vals, offsets, total, K, buckets.as<XYZZ<DF>>(),
-                       pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>(), errw.as<uint32_t>());
+                       pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>(), errw.as<uint32_t>(), fmt);
     hipLaunchKernelGGL(k_msm_fixup<DF>, dim3(blocks_for(total, 128)), dim3(128), 0, st, offsets, total, K,
                        buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>(),
-                       errw.as<uint32_t>() + 1);
+                       errw.as<uint32_t>() + 1, fmt);
   }
   // Bucket reduction, launched speculatively: buckets spanning more than
   // FIX_SERIAL slices (skewed scalars) are only known once errw[1] (max span)
@@ -661,9 +724,9 @@ int msm_run(gm_ctx* ctx, const MsmPlan& plan, const void* points_internal,
         const size_t nslices = (M + K - 1) / K;
         for (uint32_t d = 0; (1u << d) < ms; d++)
           hipLaunchKernelGGL(k_msm_fix_tree<DF>, dim3(blocks_for(nslices, 128)), dim3(128), 0, st, plan.keys,
-                             offsets, total, K, (uint32_t)nslices, d, pfirst.as<XYZZ<DF>>());
+                             plan.vals, offsets, total, K, (uint32_t)nslices, d, pfirst.as<XYZZ<DF>>(), fmt);
         hipLaunchKernelGGL(k_msm_fixup_long<DF>, dim3(blocks_for(total, 128)), dim3(128), 0, st, offsets, total,
-                           K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>());
+                           K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>(), fmt);
         GM_HIP(hipMemsetAsync(errw.as<uint32_t>() + 1, 0, 4, st));  // long spans resolved
       }
     }
@@ -676,10 +739,10 @@ int msm_run(gm_ctx* ctx, const MsmPlan& plan, const void* points_internal,
     const uint32_t K = ctx->msm_slice ? (uint32_t)ctx->msm_slice : 64u;
     const size_t nslices = (M + K - 1) / K;
     for (uint32_t d = 0; (1u << d) < maxspan; d++)
-      hipLaunchKernelGGL(k_msm_fix_tree<DF>, dim3(blocks_for(nslices, 128)), dim3(128), 0, st, plan.keys, offsets,
-                         total, K, (uint32_t)nslices, d, pfirst.as<XYZZ<DF>>());
+      hipLaunchKernelGGL(k_msm_fix_tree<DF>, dim3(blocks_for(nslices, 128)), dim3(128), 0, st, plan.keys,
+                         plan.vals, offsets, total, K, (uint32_t)nslices, d, pfirst.as<XYZZ<DF>>(), fmt);
     hipLaunchKernelGGL(k_msm_fixup_long<DF>, dim3(blocks_for(total, 128)), dim3(128), 0, st, offsets, total, K,
-                       buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>());
+                       buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>(), fmt);
     if ((rc = reduce()) || (rc = readback())) return rc;
     memcpy(&herr, stage, 4);
   }

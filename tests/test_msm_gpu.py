@@ -45,7 +45,7 @@ def test_msm_small_vs_pyref(gm_ctx, cname, g2):
     pb = b"".join(pyref.encode_point(c, p, g2) for p in pts)
     S = gm_ctx.copy_to_device(sb)
     P = gm_ctx.copy_points_to_device(cname, pb, g2)
-    for window in (0, 4, 9):
+    for window in (0, 4, 9, 16):  # 16: digit-major sort keys (KeyFmt)
         gm_ctx.set_msm_window(window)
         jac, aff = gm_ctx.msm(cname, S, P, n, g2)
         assert pyref.decode_point(c, aff, g2) == exp, (cname, g2, window)
@@ -271,4 +271,25 @@ def test_msm_bucket_chain_special_cases(gm_ctx, cname, g2):
     _, aff = gm_ctx.msm_precomputed(cname, S, pre, n, g2)
     assert pyref.decode_point(c, aff, g2) == exp
     for b in (S, P, pre):
+        b.free()
+
+
+@pytest.mark.parametrize("cname,g2,logn", [("bn254", False, 14), ("bn254", True, 12),
+                                           ("bls12377", False, 13), ("bls12377", True, 11)])
+def test_msm_digit_major_keys_vs_oracle(gm_ctx, oracle, cname, g2, logn):
+    """c = 16 (W = 16): the plan sorts by digit only and carries the window in
+    the value bits (KeyFmt); window-major (GM_MSM_DMAJOR semantics) must agree."""
+    import gnark_mi355x as gm
+    n = (1 << logn) + 11
+    S = gm_ctx.random_scalars(cname, n, seed=0x5EED0007 + logn)
+    K = gm_ctx.random_scalars(cname, n, seed=0x5EED1007 + logn)
+    P = gm_ctx.batch_mul_base(cname, g2, gm.generator(cname, g2), K, n)
+    exp = oracle.msm(cname, g2, S.to_host(), P.to_host())
+    for c in (16, 15):  # 15: W = 17 windows -> window-major keys
+        gm_ctx.set_msm_window(c)
+        try:
+            assert gm_ctx.msm(cname, S, P, n, g2)[1] == exp, c
+        finally:
+            gm_ctx.set_msm_window(0)
+    for b in (S, K, P):
         b.free()
