@@ -2,22 +2,26 @@
 // Pippenger bucket MSM on gfx950 -- replaces iciclegnark MsmOnDevice /
 // MsmG2OnDevice (backend/groth16/bn254/icicle/icicle.go:302,315,332,355,382).
 //
-// Pipeline (one HIP stream, all state in HBM):
-//   1. k_msm_hist     Montgomery -> canonical scalar, signed c-bit digits for all
-//                     W windows, histogram of (window, |digit|) buckets.
-//   2. exclusive scan of the histogram (hipcub) -> bucket offsets.
-//   3. k_msm_scatter  recompute digits, counting-sort scatter of
-//                     (point index | sign<<31) into bucket order.
-//   4. k_msm_accum    one thread per bucket: XYZZ accumulation of its points
-//                     (mixed adds, gathered affine points, sign applied on load).
-//   5. k_msm_seg      bucket reduction sum_b b*B_b, per segment of L buckets:
-//                     running sums (T_s, S_s).
-//   6. k_msm_segmul   R_s = T_s + (s*L) * S_s.
-//   7. k_msm_winsum   per-window tree reduction of R_s in LDS.
-//   8. host: Horner over windows sum_w 2^(c w) W_w (W tiny), XYZZ -> Jacobian.
+// Pipeline (one HIP stream, all state in HBM; msm_plan + msm_run below):
+//   1. k_msm_keys       Montgomery -> canonical scalar, signed c-bit digits of all
+//                       W windows -> (bucket key, point index | sign << 31) pairs;
+//                       digit-major keys (KeyFmt) when that saves a radix pass.
+//   2. radix sort of the pairs by key (msm_sort_pairs, msm_sort.hip).
+//   3. k_msm_bounds (+ k_msm_bounds_fill) or k_msm_lower_bound: bucket start
+//      offsets in the sorted list.
+//   4. k_msm_accum_seg  load-balanced slices of K sorted entries per thread:
+//                       lazily reduced XYZZ mixed adds of the gathered points
+//                       (sign applied on load); buckets cut by slice edges go to
+//                       part_first / part_last and are merged by k_msm_fixup
+//                       (k_msm_fix_tree + k_msm_fixup_long for spans > FIX_SERIAL).
+//   5. k_msm_seg        bucket reduction level 1: running sums over segments of
+//                       L buckets;  k_msm_bitsum: LDS bit-sum trees up to one node
+//                       per window;  k_msm_export: nodes -> gnark words.
+//   6. host: Horner over the window / bit-position nodes, XYZZ -> Jacobian.
+// With a precomputed point set (MsmPrecomp) every window shares one bucket set
+// and steps 5-6 run once.
 //
-// Exact group arithmetic: the result is independent of summation order, so the
-// atomics-based counting sort needs no determinism.
+// Exact group arithmetic: the result is independent of summation order.
 #include "curves.hpp"
 #include "msm.hpp"
 #include "runtime.hpp"
@@ -475,10 +479,14 @@ static __global__ void __launch_bounds__(256) k_msm_lower_bound(const uint32_t* 
   offsets[b] = lo;
 }
 
-// Digit-major keys (two loads per probe make the binary search ~2x slower): the
-// same offsets from one linear pass -- entry q (q <= M) owns the buckets b with
-// key(q-1) < b <= key(q) (key(-1) = -1, key(M) = total) -- usually one write;
-// empty buckets in a gap are written by the entry that ends it.
+// Digit-major keys (two loads per probe make a binary search per bucket ~2x
+// slower): the same offsets from one linear pass -- entry q (q <= M) owns the
+// buckets b with key(q-1) < b <= key(q) (key(-1) = -1, key(M) = total).  Gaps of
+// at most BOUNDS_GAP empty buckets are written by the entry that ends them; for
+// a longer gap (sparse keys: zero-heavy or constant scalars) the entry writes
+// only its own bucket and k_msm_bounds_fill binary-searches the rest, so no lane
+// loops over more than BOUNDS_GAP buckets.  `offsets` is preset to ~0.
+constexpr uint32_t BOUNDS_GAP = 32;
 static __global__ void __launch_bounds__(256) k_msm_bounds(const uint32_t* __restrict__ keys,
                                                     const uint32_t* __restrict__ vals, uint32_t M, uint32_t total,
                                                     uint32_t* __restrict__ offsets, KeyFmt fmt) {
@@ -486,7 +494,28 @@ static __global__ void __launch_bounds__(256) k_msm_bounds(const uint32_t* __res
   if (q > M) return;
   const uint32_t hi = q == M ? total : min(fmt.W ? fmt.key(keys[q], vals[q]) : keys[q], total);
   const uint32_t lo = q == 0 ? 0u : (fmt.W ? fmt.key(keys[q - 1], vals[q - 1]) : keys[q - 1]) + 1;
+  if (hi < lo) return;
+  if (hi - lo > BOUNDS_GAP) {
+    offsets[hi] = q;
+    return;
+  }
   for (uint32_t b = lo; b <= hi; b++) offsets[b] = q;
+}
+
+// Buckets k_msm_bounds left unset (~0): lower bound by binary search.
+static __global__ void __launch_bounds__(256) k_msm_bounds_fill(const uint32_t* __restrict__ keys,
+                                                         const uint32_t* __restrict__ vals, uint32_t M,
+                                                         uint32_t total, uint32_t* __restrict__ offsets,
+                                                         KeyFmt fmt) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b > total || offsets[b] != 0xffffffffu) return;
+  uint32_t lo = 0, hi = M;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (fmt.key(keys[mid], vals[mid]) < b) lo = mid + 1;
+    else hi = mid;
+  }
+  offsets[b] = lo;
 }
 
 // ---------------------------------------------------------------------------
@@ -585,10 +614,14 @@ int msm_plan(gm_ctx* ctx, Arena& arena, const void* scalars_dev, size_t n, const
     KeyFmt fmt;
     fmt.W = plan.dW;
     fmt.nb = plan.nb;
-    if (fmt.W)
+    if (fmt.W) {
+      GM_HIP(hipMemsetAsync(offsets.p, 0xff, sizeof(uint32_t) * (plan.total + 1), st));
       hipLaunchKernelGGL(k_msm_bounds, dim3(blocks_for(M + 1, 256)), dim3(256), 0, st, keys_out.as<uint32_t>(),
                          vals_out.as<uint32_t>(), (uint32_t)M, plan.total, offsets.as<uint32_t>(), fmt);
-    else
+      hipLaunchKernelGGL(k_msm_bounds_fill, dim3(blocks_for((size_t)plan.total + 1, 256)), dim3(256), 0, st,
+                         keys_out.as<uint32_t>(), vals_out.as<uint32_t>(), (uint32_t)M, plan.total,
+                         offsets.as<uint32_t>(), fmt);
+    } else
       hipLaunchKernelGGL(k_msm_lower_bound, dim3(blocks_for((size_t)plan.total + 1, 256)), dim3(256), 0, st,
                          keys_out.as<uint32_t>(), (uint32_t)M, plan.total, offsets.as<uint32_t>());
   }

@@ -262,6 +262,28 @@ __global__ void __launch_bounds__(256) k_bitrev_swap(Fe<P>* __restrict__ a, size
   }
 }
 
+// out[brev(i)] = in[i] (out-of-place bit-reversal permutation; out != in)
+template <class P>
+__global__ void __launch_bounds__(256) k_bitrev_copy(const Fe<P>* __restrict__ in, Fe<P>* __restrict__ out,
+                                                     size_t n, int logn) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const size_t r = brev_bits((uint32_t)i, logn);
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(in);
+  feg_store<P>(reinterpret_cast<uint32_t*>(out) + r * P::NG, feg_load<P>(src + i * P::NG));
+}
+
+// a <- (a*b - c) * den[i] with an element-wise den vector (iciclegnark PolyOps)
+template <class P>
+__global__ void __launch_bounds__(256) k_poly_ops_vec(Fe<P>* __restrict__ a, const Fe<P>* __restrict__ b,
+                                                      const Fe<P>* __restrict__ c, const Fe<P>* __restrict__ den,
+                                                      size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Fe<P> v = fe_sub(fe_mul(ld_fe(a, i), fe_to_internal(ld_fe(b, i))), ld_fe(c, i));
+  st_fe(a, i, fe_mul(v, fe_to_internal(ld_fe(den, i))));
+}
+
 // ---------------------------------------------------------------------------
 // domain (cached per context)
 // ---------------------------------------------------------------------------
@@ -556,6 +578,43 @@ int reverse_device(gm_ctx* ctx, void* a, size_t n) {
   return GM_OK;
 }
 
+template <class C>
+int bitrev_copy_device(gm_ctx* ctx, void* out, const void* in, size_t n) {
+  using Fr = typename C::Fr;
+  const int logn = log2_exact(n);
+  if (logn < 0 || out == in) {
+    set_error("bitrev_copy: n must be a power of two and out != in");
+    return GM_ERR_INVALID;
+  }
+  ProfScope ps(ctx, "bitrev");
+  hipLaunchKernelGGL(k_bitrev_copy<Fr>, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream,
+                     (const Fe<Fr>*)in, (Fe<Fr>*)out, n, logn);
+  GM_HIP(hipGetLastError());
+  return GM_OK;
+}
+
+template <class C>
+int poly_ops_vec_device(gm_ctx* ctx, void* a, const void* b, const void* c, const void* den, size_t n) {
+  using Fr = typename C::Fr;
+  ProfScope ps(ctx, "poly_ops");
+  hipLaunchKernelGGL(k_poly_ops_vec<Fr>, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream, (Fe<Fr>*)a,
+                     (const Fe<Fr>*)b, (const Fe<Fr>*)c, (const Fe<Fr>*)den, n);
+  GM_HIP(hipGetLastError());
+  return GM_OK;
+}
+
+// Builds (and caches) the domain tables of size n (GenerateTwiddleFactors).
+template <class C>
+int ntt_domain_prepare(gm_ctx* ctx, size_t n) {
+  const int logn = log2_exact(n);
+  if (logn < 0 || logn > C::TWO_ADICITY || logn > 30) {
+    set_error("ntt: n must be a power of two within the 2-adicity");
+    return GM_ERR_INVALID;
+  }
+  NttDomain<C>* d;
+  return get_domain<C>(ctx, logn, &d);
+}
+
 // computeH (prove.go:356-399; icicle.go:453-513), all scalings fused:
 //   a, b, c: INTT (DIF; 1/n folded into the top-pass twiddles) -> bit-reversed
 //            coefficients -> coset NTT (DIT; g^brev(p) applied on load) -> natural
@@ -598,7 +657,10 @@ int compute_h_device(gm_ctx* ctx, void* a, void* b, void* c, size_t len, size_t 
   template int poly_ops_device<C>(gm_ctx*, void*, const void*, const void*, size_t,        \
                                   const void*);                                           \
   template int reverse_device<C>(gm_ctx*, void*, size_t);                                 \
-  template int compute_h_device<C>(gm_ctx*, void*, void*, void*, size_t, size_t);
+  template int compute_h_device<C>(gm_ctx*, void*, void*, void*, size_t, size_t);         \
+  template int bitrev_copy_device<C>(gm_ctx*, void*, const void*, size_t);                 \
+  template int poly_ops_vec_device<C>(gm_ctx*, void*, const void*, const void*, const void*, size_t); \
+  template int ntt_domain_prepare<C>(gm_ctx*, size_t);
 GM_NTT_INST(CurveBN254)
 GM_NTT_INST(CurveBLS12377)
 

@@ -14,5 +14,13 @@ template <class C>
 int reverse_device(gm_ctx* ctx, void* a, size_t n);
 template <class C>
 int compute_h_device(gm_ctx* ctx, void* a, void* b, void* c, size_t len, size_t n);
+// out[brev(i)] = in[i] (n = 2^k, out != in)
+template <class C>
+int bitrev_copy_device(gm_ctx* ctx, void* out, const void* in, size_t n);
+// a <- (a*b - c) * den[i] (den: n device elements)
+template <class C>
+int poly_ops_vec_device(gm_ctx* ctx, void* a, const void* b, const void* c, const void* den, size_t n);
+template <class C>
+int ntt_domain_prepare(gm_ctx* ctx, size_t n);
 void ntt_domains_free(gm_ctx* ctx);
 }  // namespace gm

@@ -46,7 +46,8 @@ SYMBOLS = [
     "gm_g16_partial_bytes", "gm_g16_prove_partial", "gm_g16_finish",
     "gm_g16_pk_free", "gm_g16_prove", "gm_g16_prove_device", "gm_jac_add", "gm_jac_to_affine",
     "gm_batch_mul_base", "gm_random_scalars", "gm_generator", "gm_test_field_op",
-    "gm_test_point_op",
+    "gm_test_point_op", "gm_icicle_generate_twiddles", "gm_icicle_intt_on_device", "gm_icicle_ntt_on_device",
+    "gm_icicle_poly_ops",
 ]
 
 
@@ -111,6 +112,10 @@ def load_library(path: str = LIB_PATH):
     L.gm_generator.argtypes = [i, i, vp]
     L.gm_test_field_op.argtypes = [vp, i, i, i, vp, vp, vp, sz]
     L.gm_test_point_op.argtypes = [vp, i, i, i, vp, vp, vp, sz]
+    L.gm_icicle_generate_twiddles.argtypes = [vp, i, sz, i, pvp]
+    L.gm_icicle_intt_on_device.argtypes = [vp, i, vp, sz, i, pvp]
+    L.gm_icicle_ntt_on_device.argtypes = [vp, i, vp, vp, sz, i]
+    L.gm_icicle_poly_ops.argtypes = [vp, i, vp, vp, vp, vp, sz]
     _lib = L
     return L
 
@@ -329,6 +334,30 @@ class Context:
             _check(load_library().gm_ntt(self.handle, curve_id(curve), tmp.ptr, n, int(inverse), 0, 0))
         finally:
             tmp.free()
+
+    # ---- iciclegnark call-for-call binding (icicle.go:68-76,489-510) ----------
+    def icicle_generate_twiddle_factors(self, curve, n: int, inverse: bool) -> DeviceBuffer:
+        """GenerateTwiddleFactors: a freeable handle; the tables live in the context."""
+        p = ctypes.c_void_p()
+        _check(load_library().gm_icicle_generate_twiddles(self.handle, curve_id(curve), n, int(inverse),
+                                                          ctypes.byref(p)))
+        return DeviceBuffer(self, p.value, 64)
+
+    def icicle_intt_on_device(self, curve, scalars: DeviceBuffer, n: int, is_coset: bool) -> DeviceBuffer:
+        """INttOnDevice: natural evaluations -> NEW buffer of natural coefficients."""
+        p = ctypes.c_void_p()
+        _check(load_library().gm_icicle_intt_on_device(self.handle, curve_id(curve), scalars.ptr, n, int(is_coset),
+                                                       ctypes.byref(p)))
+        return DeviceBuffer(self, p.value, FR_BYTES * n)
+
+    def icicle_ntt_on_device(self, curve, out: DeviceBuffer, scalars: DeviceBuffer, n: int, is_coset: bool):
+        """NttOnDevice(out, in): natural coefficients -> natural evaluations in out."""
+        _check(load_library().gm_icicle_ntt_on_device(self.handle, curve_id(curve), out.ptr, scalars.ptr, n,
+                                                      int(is_coset)))
+
+    def icicle_poly_ops(self, curve, a: DeviceBuffer, b: DeviceBuffer, c: DeviceBuffer, den: DeviceBuffer, n: int):
+        """PolyOps(a, b, c, den_d, n) with a device den vector."""
+        _check(load_library().gm_icicle_poly_ops(self.handle, curve_id(curve), a.ptr, b.ptr, c.ptr, den.ptr, n))
 
     def poly_ops(self, curve, a: DeviceBuffer, b: DeviceBuffer, c: DeviceBuffer, n: int, den: bytes):
         d = _buf(den)

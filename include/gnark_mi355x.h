@@ -134,6 +134,32 @@ int gm_poly_ops(gm_ctx* ctx, int curve, void* a_dev, const void* b_dev, const vo
 /* In-place bit-reversal permutation of n = 2^k Fr elements (ReverseScalars). */
 int gm_reverse_scalars(gm_ctx* ctx, int curve, void* data_dev, size_t n);
 
+/* ---- iciclegnark call-for-call binding (icicle.go:68-76,489-510) --------
+ * Same buffer ownership and element order as iciclegnark v0.1.0, so a cgo shim
+ * can bind INttOnDevice / NttOnDevice / PolyOps / GenerateTwiddleFactors name
+ * for name and icicle.go's computeH (icicle.go:453-513) runs unchanged,
+ * including its FreeDevicePointer calls:
+ *  - gm_icicle_intt_on_device: natural-order evaluations at in_dev -> a NEW
+ *    device buffer (*out_dev, free with gm_free) of natural-order coefficients
+ *    (times g^-i / n on the coset); in_dev is left bit-reversed, as iciclegnark
+ *    leaves it (INttOnDevice, icicle.go:489,502).
+ *  - gm_icicle_ntt_on_device: natural-order coefficients at in_dev -> natural-
+ *    order evaluations (on the coset g*w^i if coset) at out_dev (NttOnDevice,
+ *    icicle.go:490); out_dev == in_dev is allowed.
+ *  - gm_icicle_poly_ops: a[i] <- (a[i]*b[i] - c[i]) * den[i], den a device
+ *    vector (PolyOps with pk.DenDevice, icicle.go:52-65,500).
+ *  - gm_icicle_generate_twiddles: builds the context's cached domain of size n
+ *    and returns a freeable device token for pk.DomainDevice.Twiddles(Inv)
+ *    (GenerateTwiddleFactors, icicle.go:68,73).
+ * ReverseScalars (icicle.go:510) is gm_reverse_scalars, MsmOnDevice /
+ * MsmG2OnDevice are gm_msm, CopyToDevice / CopyPointsToDevice are
+ * gm_copy_to_device / gm_copy_points_to_device, FreeDevicePointer is gm_free. */
+int gm_icicle_generate_twiddles(gm_ctx* ctx, int curve, size_t n, int inverse, void** token_out);
+int gm_icicle_intt_on_device(gm_ctx* ctx, int curve, void* in_dev, size_t n, int coset, void** out_dev);
+int gm_icicle_ntt_on_device(gm_ctx* ctx, int curve, void* out_dev, const void* in_dev, size_t n, int coset);
+int gm_icicle_poly_ops(gm_ctx* ctx, int curve, void* a_dev, const void* b_dev, const void* c_dev,
+                       const void* den_dev, size_t n);
+
 /* ---- Groth16 computeH (icicle.go:453-513; prove.go:356-399) -----------
  * a, b, c: `len` Montgomery fr.Elements each (the R1CS solution vectors),
  * device-resident, zero-padded in place to n = domain size (buffers must hold

@@ -20,6 +20,13 @@ FR_BYTES = 32
 
 _lib = None
 
+# Host threads the checker uses: the CPUs this process may run on, at most 16
+# (a one-GPU box's CPU share; os.cpu_count() there reports the whole machine).
+try:
+    NTHREADS = max(1, min(16, len(os.sched_getaffinity(0))))
+except AttributeError:  # pragma: no cover
+    NTHREADS = max(1, min(16, os.cpu_count() or 1))
+
 
 def build():
     subprocess.check_call(["make", "-s", "-C", HERE])
@@ -59,7 +66,8 @@ def point_bytes(curve: str, g2: bool) -> int:
     return FP_BYTES[curve] * (4 if g2 else 2)
 
 
-def msm(curve: str, g2: bool, scalars, points, nthreads: int = 8, naive: bool = False) -> bytes:
+def msm(curve: str, g2: bool, scalars, points, nthreads: int = 0, naive: bool = False) -> bytes:
+    nthreads = nthreads or NTHREADS
     s = _u8(scalars)
     p = _u8(points)
     n = s.size // FR_BYTES
@@ -70,7 +78,8 @@ def msm(curve: str, g2: bool, scalars, points, nthreads: int = 8, naive: bool = 
     return out.tobytes()
 
 
-def fft(curve: str, data, inverse: bool, dit: bool, coset: bool, nthreads: int = 8) -> bytes:
+def fft(curve: str, data, inverse: bool, dit: bool, coset: bool, nthreads: int = 0) -> bytes:
+    nthreads = nthreads or NTHREADS
     a = _u8(data).copy()
     n = a.size // FR_BYTES
     rc = lib().o_fft(CURVE_ID[curve], _ptr(a), n, int(inverse), int(dit), int(coset), nthreads)
@@ -78,7 +87,8 @@ def fft(curve: str, data, inverse: bool, dit: bool, coset: bool, nthreads: int =
     return a.tobytes()
 
 
-def compute_h(curve: str, a, b, c, n: int, nthreads: int = 8) -> bytes:
+def compute_h(curve: str, a, b, c, n: int, nthreads: int = 0) -> bytes:
+    nthreads = nthreads or NTHREADS
     A, B, C = _u8(a), _u8(b), _u8(c)
     ln = A.size // FR_BYTES
     out = np.zeros(n * FR_BYTES, dtype=np.uint8)
@@ -92,7 +102,8 @@ def generator(curve: str, g2: bool) -> bytes:
     return bytes(p[: point_bytes(curve, g2)])
 
 
-def batch_mul_base(curve: str, g2: bool, base: bytes, scalars, nthreads: int = 8) -> bytes:
+def batch_mul_base(curve: str, g2: bool, base: bytes, scalars, nthreads: int = 0) -> bytes:
+    nthreads = nthreads or NTHREADS
     s = _u8(scalars)
     n = s.size // FR_BYTES
     b = _u8(base)
@@ -111,8 +122,9 @@ def _ptr_array(arrs):
     return ptrs, keep
 
 
-def g16_setup(curve: str, r1cs, toxic: bytes, nthreads: int = 8):
+def g16_setup(curve: str, r1cs, toxic: bytes, nthreads: int = 0):
     """Returns a dict with the proving-key arrays (gnark layout bytes)."""
+    nthreads = nthreads or NTHREADS
     fpb = FP_BYTES[curve]
     g1b, g2b = 2 * fpb, 4 * fpb
     n = r1cs.domain_size
@@ -142,7 +154,8 @@ def g16_setup(curve: str, r1cs, toxic: bytes, nthreads: int = 8):
     return pk
 
 
-def g16_prove(curve: str, pk, nb_public: int, wires, a, b, c, r: bytes, s: bytes, nthreads: int = 8):
+def g16_prove(curve: str, pk, nb_public: int, wires, a, b, c, r: bytes, s: bytes, nthreads: int = 0):
+    nthreads = nthreads or NTHREADS
     fpb = FP_BYTES[curve]
     g1, k4 = _ptr_array([pk[k] for k in ["g1_alpha", "g1_beta", "g1_delta", "g1_A", "g1_B", "g1_Z", "g1_K"]])
     g2, k5 = _ptr_array([pk[k] for k in ["g2_beta", "g2_delta", "g2_B"]])

@@ -103,3 +103,50 @@ def squaring_chain(k: int, curve: str = "bn254", x: int = 2):
 def encode_vec(curve: str, vals) -> bytes:
     c = pyref.CURVES[curve]
     return b"".join(pyref.encode_fr(c, v) for v in vals)
+
+
+class R1CSArrays:
+    """R1CS in the CSR form the oracle consumes (same attributes as R1CS),
+    built directly from numpy arrays -- for circuits with ~2^20 constraints,
+    where the per-constraint Python lists of R1CS are too slow."""
+
+    def __init__(self, curve, nb_public, nb_wires, nc, rowptr, wires, coeffs, nbA, nbB):
+        self.curve = curve
+        self.c = pyref.CURVES[curve]
+        self.nb_public, self.nb_wires, self.nc = nb_public, nb_wires, nc
+        n = 1
+        while n < nc:
+            n <<= 1
+        self.domain_size = n
+        self.rowptr, self.wires, self.coeffs = rowptr, wires, coeffs
+        self.nbA, self.nbB = nbA, nbB
+
+
+def squaring_chain_fast(k: int, curve: str = "bn254", x: int = 2):
+    """squaring_chain(k) (groth16_test.go:120-156 refCircuit) as R1CSArrays plus
+    the encoded solution: returns (r1, W, a, b, c), the last four as gnark-layout
+    Montgomery bytes (W: nb_wires Fr; a, b, c: nc Fr each = solution.A/B/C)."""
+    c = pyref.CURVES[curve]
+    nc = k + 1
+    one = pyref.encode_fr(c, 1)
+    j = np.arange(k, dtype=np.uint32)
+    rp = np.arange(nc + 1, dtype=np.uint32)  # exactly one term per row in L, R and O
+    wl = np.concatenate([2 + j, np.array([0], np.uint32)])
+    wr = np.concatenate([2 + j, np.array([2 + k], np.uint32)])
+    wo = np.concatenate([3 + j, np.array([1], np.uint32)])
+    co = np.frombuffer(one * nc, np.uint8).copy()
+    r1 = R1CSArrays(curve, 2, 3 + k, nc, [rp, rp.copy(), rp.copy()], [wl, wr, wo], [co, co.copy(), co.copy()],
+                    nbA=k + 1, nbB=k + 1)
+    R = (1 << 256) % c.r
+    v = x % c.r
+    vals = [1, 0, v]
+    for _ in range(k):
+        v = v * v % c.r
+        vals.append(v)
+    vals[1] = v
+    W = b"".join((u * R % c.r).to_bytes(32, "little") for u in vals)
+    Wa = np.frombuffer(W, np.uint8).reshape(-1, 32)
+    a = np.concatenate([Wa[2:2 + k], Wa[0:1]]).tobytes()
+    b = np.concatenate([Wa[2:2 + k], Wa[2 + k:3 + k]]).tobytes()
+    cc = np.concatenate([Wa[3:3 + k], Wa[1:2]]).tobytes()
+    return r1, W, a, b, cc

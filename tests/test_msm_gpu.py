@@ -54,19 +54,59 @@ def test_msm_small_vs_pyref(gm_ctx, cname, g2):
     P.free()
 
 
+@pytest.mark.parametrize("window", [0, 16])  # 16: digit-major plan (KeyFmt)
 @pytest.mark.parametrize("cname,g2", CASES)
-def test_msm_empty_and_single(gm_ctx, cname, g2):
+def test_msm_empty_and_single(gm_ctx, cname, g2, window):
     import gnark_mi355x as gm
     c = pyref.CURVES[cname]
     P0 = pyref.random_points(c, 1, 5, g2)[0]
     S = gm_ctx.copy_to_device(pyref.encode_fr(c, 12345))
     P = gm_ctx.copy_points_to_device(cname, pyref.encode_point(c, P0, g2), g2)
-    _, aff = gm_ctx.msm(cname, S, P, 0, g2)
-    assert aff == bytes(gm.point_bytes(cname, g2))  # empty MSM = infinity
-    _, aff = gm_ctx.msm(cname, S, P, 1, g2)
-    assert pyref.decode_point(c, aff, g2) == pyref.Group(c, g2).mul(P0, 12345)
-    S.free()
+    gm_ctx.set_msm_window(window)
+    try:
+        _, aff = gm_ctx.msm(cname, S, P, 0, g2)
+        assert aff == bytes(gm.point_bytes(cname, g2))  # empty MSM = infinity
+        _, aff = gm_ctx.msm(cname, S, P, 1, g2)
+        assert pyref.decode_point(c, aff, g2) == pyref.Group(c, g2).mul(P0, 12345)
+    finally:
+        gm_ctx.set_msm_window(0)
+        S.free()
+        P.free()
+
+
+@pytest.mark.parametrize("value", [0, 1, "r-1"])
+@pytest.mark.parametrize("cname,g2", [("bn254", False), ("bls12377", True)])
+def test_msm_constant_scalars_c16(gm_ctx, oracle, cname, g2, value):
+    """All scalars equal at c = 16 (digit-major offsets, msm_plan): 0 (every
+    entry is a zero digit -- all buckets empty), 1 (one bucket, all others empty)
+    and r-1 (every window's top digit)."""
+    import gnark_mi355x as gm
+    c = pyref.CURVES[cname]
+    n = (1 << 14) + 3
+    v = c.r - 1 if value == "r-1" else value
+    sb = pyref.encode_fr(c, v) * n
+    pb = _random_points_host(gm_ctx, cname, g2, n, 0x77 + g2)
+    S = gm_ctx.copy_to_device(sb)
+    P = gm_ctx.copy_to_device(pb)
+    exp = oracle.msm(cname, g2, sb, pb)
+    try:
+        for window in (16, 0):
+            gm_ctx.set_msm_window(window)
+            assert gm_ctx.msm(cname, S, P, n, g2)[1] == exp, window
+    finally:
+        gm_ctx.set_msm_window(0)
+        S.free()
+        P.free()
+
+
+def _random_points_host(ctx, cname, g2, n, seed):
+    import gnark_mi355x as gm
+    K = ctx.random_scalars(cname, n, seed)
+    P = ctx.batch_mul_base(cname, g2, gm.generator(cname, g2), K, n)
+    out = P.to_host()
+    K.free()
     P.free()
+    return out
 
 
 def test_msm_all_equal_points(gm_ctx, oracle):
@@ -240,8 +280,9 @@ def test_msm_precomputed_large_matches_plain(gm_ctx):
         b.free()
 
 
+@pytest.mark.parametrize("window", [0, 16])
 @pytest.mark.parametrize("cname,g2", CASES)
-def test_msm_bucket_chain_special_cases(gm_ctx, cname, g2):
+def test_msm_bucket_chain_special_cases(gm_ctx, cname, g2, window):
     """Within one bucket the accumulator meets -(running sum) (-> infinity) and
     +(running sum) (-> doubling) after several adds, i.e. while its coordinates
     are non-canonical (lazily reduced G1 accumulation, field.hpp).  All scalars
@@ -265,9 +306,13 @@ def test_msm_bucket_chain_special_cases(gm_ctx, cname, g2):
     exp = G.msm([1] * n, pts)
     S = gm_ctx.copy_to_device(sb)
     P = gm_ctx.copy_points_to_device(cname, pb, g2)
-    _, aff = gm_ctx.msm(cname, S, P, n, g2)
+    gm_ctx.set_msm_window(window)
+    try:
+        _, aff = gm_ctx.msm(cname, S, P, n, g2)
+    finally:
+        gm_ctx.set_msm_window(0)
     assert pyref.decode_point(c, aff, g2) == exp
-    pre = gm_ctx.points_upload_precomputed(cname, pb, g2, 0)
+    pre = gm_ctx.points_upload_precomputed(cname, pb, g2, window)
     _, aff = gm_ctx.msm_precomputed(cname, S, pre, n, g2)
     assert pyref.decode_point(c, aff, g2) == exp
     for b in (S, P, pre):
