@@ -64,6 +64,16 @@ def load_pmc_traffic(name):
         return None
 
 
+def load_pmc_valu(name):
+    """VALU utilisation of a kernel from the committed PMC summary (or None)."""
+    p = os.path.join(ROOT, "profiles", "r02_pmc_valu.json")
+    try:
+        with open(p) as f:
+            return json.load(f).get(name)
+    except (OSError, ValueError):
+        return None
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -88,6 +98,7 @@ def main():
     K = ctx.random_scalars("bn254", n, 0x5EED1002 + rank)
     P = ctx.batch_mul_base("bn254", False, gm.generator("bn254"), K, n)
     K.free()
+    add_edge_set(ctx, gm, S, P, n)
     ctx.synchronize()
 
     def barrier():
@@ -142,9 +153,11 @@ def main():
         "int_alu": {"achieved": round(tmads, 3), "peak": round(MAD_PEAK_T, 2), "unit": "T v_mad_u64_u32/s",
                     "frac": round(tmads / MAD_PEAK_T, 4),
                     "work": "%d points x %d windows XYZZ mixed adds x %d mads" % (n, windows, MADS_PER_MIXED_ADD)},
-        "note": "MSM bucket accumulation is bound by VALU issue (v_mad_u64_u32 plus the carry/mask "
-                "instructions of the radix-2^29 products; no MFMA, HBM well below peak): int_alu is the binding "
-                "roofline, priced at the measured mad-only issue peak (DESIGN.md section 3)",
+        "valu": load_pmc_valu("k_msm_accum_seg<Fe<Bn254Fp> >"),
+        "note": "bound=hbm is the bench contract's roofline for this non-MFMA path; the kernel is NOT HBM-bound: "
+                "its binding resource is VALU issue -- rocprofv3 PMC (profiles/r02_pmc_valu.json) shows VALUBusy "
+                "~0.88 (gfx9 formula, 4 cycles/instr) for k_msm_accum_seg, ~2880 VALU instructions per mixed add; "
+                "int_alu prices the v_mad_u64_u32 work at the measured mad-only issue peak (DESIGN.md section 3)",
     }
     kernel_ms = {k: round(v[0] / max(v[1], 1), 4) for k, v in stats.items()}
 
@@ -173,6 +186,12 @@ def main():
         g = groth16_sharded_bench(ctx, gm, args.g16_sharded_logn, rank, world, dist, torch)
         if rank == 0:
             out["secondary"] = {"groth16_sharded": g}
+        # the single-process seam gnark's groth16.Prove uses: rank 0 drives all
+        # N GPUs through gm_multi while the other ranks wait at the barrier
+        barrier()
+        if rank == 0:
+            out["secondary"]["groth16_multi"] = groth16_multi_bench(ctx, gm, args.g16_sharded_logn, world)
+        barrier()
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(S, P, n, res)
     if rank == 0:
@@ -180,6 +199,24 @@ def main():
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+R_BN254 = 21888242871839275222246405745257275088548364400416034343698204186575808495617
+
+
+def add_edge_set(ctx, gm, S, P, n):
+    """BASELINE.md §2.2 edge sets inside the config-2 input: 1% of the points at
+    infinity ((0,0), every 100th), a run of 1% all-equal points (DummySetup
+    shape, setup.go:544-558) and scalars 0, 1, r-1."""
+    import numpy as np
+    if n < 1024:
+        return
+    pb = np.frombuffer(P.to_host(), np.uint8).reshape(n, 64).copy()
+    pb[::100] = 0
+    pb[n // 2:n // 2 + n // 100] = pb[1]
+    P.write(pb.tobytes())
+    enc = lambda v: (v * (1 << 256) % R_BN254).to_bytes(32, "little")
+    S.write(enc(0) + enc(1) + enc(R_BN254 - 1), offset=32 * 7)
 
 
 def secondary(ctx, gm, args):
@@ -219,7 +256,7 @@ def secondary(ctx, gm, args):
         res["groth16"] = []
         for l in (int(x) for x in args.g16_logn.split(",") if x):
             if l in plain:
-                res["groth16"].append(groth16_bench(ctx, gm, l, precompute=False))
+                res["groth16"].append(groth16_bench(ctx, gm, l, precompute=False, check_oracle=(l <= 20)))
             res["groth16"].append(groth16_bench(ctx, gm, l, precompute=True))
     return res
 
@@ -250,49 +287,88 @@ def msm_line(ctx, gm, curve, g2, logn, reps=5, precompute=False):
     return {"mpoints_per_s": round(n / dt / 1e6, 3), "ms": round(dt * 1e3, 3)}
 
 
-def groth16_bench(ctx, gm, logn, precompute=True):
-    """Groth16 prove at n = 2^logn with a synthetic proving key (random points,
-    the DummySetup-style timing setup of groth16_test.go:70-88) and synthetic
-    solution vectors; timer scope = icicle.go:204-412 (after Solve)."""
+def synthetic_pk(ctx, gm, n, nb_wires, nb_public, slices=None):
+    """Synthetic proving key of random points (the DummySetup-style timing key of
+    groth16_test.go:70-88; a real setup at 2^24 is out of reach here).  slices:
+    {array: (lo, hi)} keeps only those slices (sharded keys)."""
+    import numpy as np
+    gen1, gen2 = gm.generator("bn254", False), gm.generator("bn254", True)
+
+    def pts(count, g2, seed):
+        if count <= 0:
+            return np.zeros(0, np.uint8)
+        k = ctx.random_scalars("bn254", count, seed)
+        p = ctx.batch_mul_base("bn254", g2, gen2 if g2 else gen1, k, count)
+        b = np.frombuffer(p.to_host(), np.uint8)
+        k.free()
+        p.free()
+        return b
+
+    cnt = {"g1_A": nb_wires, "g1_B": nb_wires, "g1_Z": n - 1, "g1_K": nb_wires - nb_public, "g2_B": nb_wires}
+    sd = {"g1_A": 3, "g1_B": 4, "g1_Z": 5, "g1_K": 6, "g2_B": 7}
+    one1 = pts(3, False, 1)
+    one2 = pts(2, True, 2)
+    pk = {"g1_alpha": one1[:64], "g1_beta": one1[64:128], "g1_delta": one1[128:192],
+          "g2_beta": one2[:128], "g2_delta": one2[128:256],
+          "infA": np.zeros(nb_wires, np.uint8), "infB": np.zeros(nb_wires, np.uint8)}
+    for k, c in cnt.items():
+        lo, hi = slices[k] if slices else (0, c)
+        pk[k] = pts(hi - lo, k == "g2_B", 1000 * (lo + 1) + sd[k] if slices else sd[k])
+    return pk
+
+
+def groth16_bench(ctx, gm, logn, precompute=True, check_oracle=False):
+    """Groth16 prove at n = 2^logn (synthetic pk of random points, synthetic
+    solution vectors), timed in two scopes:
+      host:   wires / a / b / c in host memory, gm_g16_prove -- the scope of
+              icicle.go:204-412 (its H2D copies of a, b, c and wA / wB included);
+      device: the same vectors already resident (gm_g16_prove_device).
+    check_oracle: the timed host-scope proof is compared with the oracle prover
+    (prove.go:62-325 restatement) on the same key and inputs."""
     import numpy as np
     n = 1 << logn
     nb_wires = n + 2
     nb_public = 2
-    gen1, gen2 = gm.generator("bn254", False), gm.generator("bn254", True)
-
-    def pts(count, g2, seed):
-        k = ctx.random_scalars("bn254", count, seed)
-        p = ctx.batch_mul_base("bn254", g2, gen2 if g2 else gen1, k, count)
-        b = p.to_host()
-        k.free()
-        p.free()
-        return np.frombuffer(b, np.uint8)
-
-    one1 = pts(3, False, 1)
-    one2 = pts(2, True, 2)
-    pk = {"g1_alpha": one1[:64], "g1_beta": one1[64:128], "g1_delta": one1[128:192],
-          "g1_A": pts(nb_wires, False, 3), "g1_B": pts(nb_wires, False, 4), "g1_Z": pts(n - 1, False, 5),
-          "g1_K": pts(nb_wires - nb_public, False, 6), "g2_beta": one2[:128], "g2_delta": one2[128:256],
-          "g2_B": pts(nb_wires, True, 7), "infA": np.zeros(nb_wires, np.uint8), "infB": np.zeros(nb_wires, np.uint8)}
+    pk = synthetic_pk(ctx, gm, n, nb_wires, nb_public)
     dpk = gm.ProvingKey(ctx, "bn254", pk, n, nb_wires, nb_public, precompute=precompute)
-    del pk
     W = ctx.random_scalars("bn254", nb_wires, 8)
-    A, B, C = (ctx.malloc(32 * n) for _ in range(3))
     srcs = [ctx.random_scalars("bn254", n, 9 + i) for i in range(3)]
     r = ctx.random_scalars("bn254", 2, 12).to_host()
-    times = []
-    for it in range(3 if logn < 24 else 2):
+    host = [np.frombuffer(x.to_host(), np.uint8) for x in [W] + srcs]
+    A, B, C = (ctx.malloc(32 * n) for _ in range(3))
+    reps = 3 if logn < 24 else 2
+    t_dev, t_host = [], []
+    for _ in range(reps):
         for dst, src in zip((A, B, C), srcs):
             dst.copy_from(src)
         ctx.synchronize()
         t0 = time.perf_counter()
         dpk.prove_device(W, A, B, C, n, r[:32], r[32:])
-        times.append(time.perf_counter() - t0)
+        t_dev.append(time.perf_counter() - t0)
+    proof = None
+    for _ in range(reps):
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        proof = dpk.prove(host[0], host[1], host[2], host[3], r[:32], r[32:])
+        t_host.append(time.perf_counter() - t0)
     dpk.free()
     for b in [W, A, B, C] + srcs:
         b.free()
-    return {"logn": logn, "prove_ms": round(min(times) * 1e3, 3), "pk": "precomputed" if precompute else "plain",
-            "note": "inputs device-resident; after Solve"}
+    med = lambda v: sorted(v)[len(v) // 2]
+    res = {"logn": logn, "pk": "precomputed" if precompute else "plain",
+           "prove_ms_host_inputs": round(med(t_host) * 1e3, 3), "prove_ms_device_inputs": round(med(t_dev) * 1e3, 3),
+           "runs": reps, "stat": "median",
+           "scope": "host_inputs = icicle.go:204-412 incl. H2D of wires/a/b/c; device_inputs = same with inputs "
+                    "resident; both after Solve"}
+    if check_oracle:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle_lib
+        pk["sizes"] = np.array([n, nb_wires, nb_wires, nb_wires, nb_wires - nb_public], np.uint64)
+        t0 = time.perf_counter()
+        exp = oracle_lib.g16_prove("bn254", pk, nb_public, host[0], host[1], host[2], host[3], r[:32], r[32:])
+        res["oracle_s"] = round(time.perf_counter() - t0, 2)
+        res["matches_oracle"] = bool(exp == proof)
+    return res
 
 
 def groth16_sharded_bench(ctx, gm, logn, rank, world, dist, torch):
@@ -364,11 +440,61 @@ def groth16_sharded_bench(ctx, gm, logn, rank, world, dist, torch):
             "note": "computeH replicated per rank; 5 MSMs sharded; partials all-gathered over RCCL; after Solve"}
 
 
+def host_cpu():
+    """(threads this process may use, CPU model string)."""
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return cores, model
+
+
+def groth16_multi_bench(ctx, gm, logn, ndev, precompute=True):
+    """BASELINE config 4 through the single-process multi-device C-ABI
+    (gm_g16_prove_multi): one host thread per GPU, key sharded across GPUs
+    0..ndev-1, wire slices / a, b, c to device 0 / h slices over xGMI, host
+    inputs (icicle.go:204-412 scope incl. H2D)."""
+    import numpy as np
+    n = 1 << logn
+    nb_wires, nb_public = n + 2, 2
+    pk = synthetic_pk(ctx, gm, n, nb_wires, nb_public)
+    vecs = [ctx.random_scalars("bn254", m, 8 + i) for i, m in enumerate((nb_wires, n, n, n))]
+    host = [np.frombuffer(v.to_host(), np.uint8) for v in vecs]
+    for v in vecs:
+        v.free()
+    r = ctx.random_scalars("bn254", 2, 12).to_host()
+    nvis = gm.device_count()  # < ndev only in the one-GPU gloo rehearsal
+    with gm.Multi([d % nvis for d in range(ndev)]) as m:
+        t0 = time.perf_counter()
+        mpk = gm.ProvingKeyMulti(m, "bn254", pk, n, nb_wires, nb_public, precompute=precompute)
+        t_up = time.perf_counter() - t0
+        times = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            mpk.prove(host[0], host[1], host[2], host[3], r[:32], r[32:])
+            times.append(time.perf_counter() - t0)
+        mpk.free()
+    return {"logn": logn, "n_gpus": ndev, "prove_ms_host_inputs": round(sorted(times)[1] * 1e3, 3), "runs": 3,
+            "stat": "median", "pk_upload_s": round(t_up, 2), "pk": "precomputed" if precompute else "plain",
+            "note": "one process, one host thread per GPU (gm_multi); computeH on GPU 0, h slices peer-copied"}
+
+
 def cpu_baseline(S, P, n, gpu_jac):
-    """Oracle C++ Pippenger (the 'port') on the host, same 2^logn workload."""
+    """Oracle C++ Pippenger (the 'port') on the host cores this process may use
+    (the box's CPU share), same 2^logn workload incl. the edge set, checked
+    against the GPU result."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_lib
-    threads = min(16, os.cpu_count() or 1)
+    threads, model = host_cpu()
     sb, pb = S.to_host(), P.to_host()
     oracle_lib.msm("bn254", False, sb[: 32 * 1024], pb[: 64 * 1024], nthreads=threads)  # warm
     t0 = time.perf_counter()
@@ -382,7 +508,9 @@ def cpu_baseline(S, P, n, gpu_jac):
     import gnark_mi355x as gm
     match = gm.jac_to_affine("bn254", False, gpu_jac) == aff
     return {"value": round(n / dt / 1e6, 4), "unit": "Mpoints/s", "cores": threads, "kind": "port",
-            "sample": "full 2^%d-point BN254 G1 MSM, %d rep(s), C++ Pippenger restatement (oracle/), not gnark-crypto"
+            "cpu_model": model,
+            "sample": "full 2^%d-point BN254 G1 MSM (same input, edge set incl.), %d rep(s), C++ Pippenger "
+                      "restatement (oracle/), not gnark-crypto (no Go toolchain on the box)"
                       % (n.bit_length() - 1, reps),
             "result_matches_gpu": bool(match)}
 

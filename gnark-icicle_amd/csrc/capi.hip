@@ -1,8 +1,6 @@
-// C-ABI implementation (include/gnark_mi355x.h) and the Groth16 prover
-// orchestration that replaces icicle_bn254.Prove
-// (backend/groth16/bn254/icicle/icicle.go:133-422), re-derived from the current
-// CPU prover groth16_bn254.Prove (backend/groth16/bn254/prove.go:62-325) as
-// SURVEY.md §0.3 prescribes: only the MSMs and NTTs move to the device.
+// C-ABI implementation (include/gnark_mi355x.h): context, memory, MSM, KZG,
+// NTT / computeH, host group helpers and synthetic inputs.  The Groth16 prover
+// entry points live in groth16.hip.
 #include <cstdlib>
 #include <cstring>
 #include <thread>
@@ -83,16 +81,6 @@ __global__ void __launch_bounds__(128) k_batch_mul_base(const uint32_t* __restri
   store_affine_gnark<F>(out + i * 2 * Coord<F>::WORDS, r);
 }
 
-// dst[i] = src[idx[i]] (Fr, 32 bytes) -- device-side scalar compaction
-__global__ void k_gather_fr(const uint4* __restrict__ src, const uint32_t* __restrict__ idx, size_t n,
-                            uint4* __restrict__ dst) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const size_t j = idx[i];
-  dst[2 * i] = src[2 * j];
-  dst[2 * i + 1] = src[2 * j + 1];
-}
-
 // ---------------------------------------------------------------------------
 // dispatch helpers
 // ---------------------------------------------------------------------------
@@ -119,30 +107,22 @@ static int check_curve(int curve) {
   return GM_OK;
 }
 
-static size_t fp_bytes(int curve) { return curve == GM_BN254 ? 32 : 48; }
+size_t fp_bytes(int curve) { return curve == GM_BN254 ? 32 : 48; }
 
 }  // namespace gm
 
 using namespace gm;
 
-// ===========================================================================
-// Groth16 proving key on device
-// ===========================================================================
-struct gm_g16_pk {
-  int curve;
-  size_t n, nb_wires, nb_public, nbA, nbB, nbK;
-  void *A, *B, *Z, *K, *B2;       // device point arrays
-  void *idxA, *idxB, *idxK;       // device index maps (compaction)
-  size_t zlo = 0, nbZ = 0;        // this shard's slice of h / pk.G1.Z (whole: 0, n-1)
-  bool precomp = false;           // GM_PK_PRECOMPUTE: fixed-base window copies
-  MsmPrecomp preA, preB, preZ, preK;  // layouts (B and B2 share preB)
-  std::vector<uint8_t> alpha, beta, delta, beta2, delta2;  // host affine
-};
-
 extern "C" {
 
 const char* gm_last_error(void) { return g_last_error.c_str(); }
-int gm_version(void) { return 1; }
+int gm_version(void) { return 2; }
+
+int gm_device_count(int* count) {
+  if (!count) return GM_ERR_INVALID;
+  GM_HIP(hipGetDeviceCount(count));
+  return GM_OK;
+}
 
 int gm_init(int device, gm_ctx** out) {
   if (!out) return GM_ERR_INVALID;
@@ -159,6 +139,7 @@ int gm_init(int device, gm_ctx** out) {
   if (const char* sl = getenv("GM_MSM_SLICE")) c->msm_slice = atoi(sl) > 0 ? atoi(sl) : 0;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
   if (e != hipSuccess) {
     set_error(std::string("hipStreamCreate: ") + hipGetErrorString(e));
     delete c;
@@ -173,6 +154,7 @@ int gm_destroy(gm_ctx* ctx) {
   hipSetDevice(ctx->device);
   hipStreamSynchronize(ctx->stream);
   if (ctx->aux) hipStreamSynchronize(ctx->aux);
+  if (ctx->copy) hipStreamSynchronize(ctx->copy);
   ntt_domains_free(ctx);
   for (auto& ch : ctx->chunks) hipFree(ch.base);
   ctx->chunks.clear();
@@ -183,6 +165,7 @@ int gm_destroy(gm_ctx* ctx) {
   }
   hipStreamDestroy(ctx->stream);
   if (ctx->aux) hipStreamDestroy(ctx->aux);
+  if (ctx->copy) hipStreamDestroy(ctx->copy);
   if (ctx->pinned) hipHostFree(ctx->pinned);
   delete ctx;
   return GM_OK;
@@ -629,497 +612,4 @@ int gm_batch_mul_base(gm_ctx* ctx, int curve, int g2, const void* base, const vo
             : batch_mul_t<CurveBLS12377, false>(ctx, base, sc, n, out);
 }
 
-// ---- Groth16 ------------------------------------------------------------------------------
-int gm_g16_pk_upload(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, gm_g16_pk** out) {
-  return gm_g16_pk_upload_ex(ctx, curve, h, 0u, out);
-}
-
-int gm_g16_pk_upload_ex(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsigned flags, gm_g16_pk** out) {
-  return gm_g16_pk_upload_shard(ctx, curve, h, flags, 0, 1, out);
-}
-
-// [lo, hi) of rank's contiguous shard of n items (gnark_mi355x.shard_range)
-static void shard_of(size_t n, int rank, int world, size_t* lo, size_t* hi) {
-  const size_t q = n / (size_t)world, r = n % (size_t)world;
-  *lo = (size_t)rank * q + std::min((size_t)rank, r);
-  *hi = *lo + q + ((size_t)rank < r ? 1 : 0);
-}
-
-int gm_g16_pk_upload_shard(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsigned flags, int rank, int world,
-                           gm_g16_pk** out) {
-  if (int rc = check_curve(curve)) return rc;
-  if (flags & ~(unsigned)GM_PK_PRECOMPUTE) {
-    set_error("pk upload: unknown flags");
-    return GM_ERR_INVALID;
-  }
-  if (!h || !out || h->domain_size < 2) return GM_ERR_INVALID;
-  if (world < 1 || rank < 0 || rank >= world) {
-    set_error("pk upload: bad rank / world");
-    return GM_ERR_INVALID;
-  }
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
-  GM_HIP(hipSetDevice(ctx->device));
-  auto* pk = new gm_g16_pk();
-  pk->curve = curve;
-  pk->n = h->domain_size;
-  pk->nb_wires = h->nb_wires;
-  pk->nb_public = h->nb_public;
-  size_t loA, hiA, loB, hiB, loK, hiK, loZ, hiZ;
-  shard_of(h->nbA, rank, world, &loA, &hiA);
-  shard_of(h->nbB, rank, world, &loB, &hiB);
-  shard_of(h->nbK, rank, world, &loK, &hiK);
-  shard_of(pk->n - 1, rank, world, &loZ, &hiZ);
-  pk->nbA = hiA - loA;
-  pk->nbB = hiB - loB;
-  pk->nbK = hiK - loK;
-  pk->zlo = loZ;
-  pk->nbZ = hiZ - loZ;
-  pk->precomp = (flags & GM_PK_PRECOMPUTE) != 0;
-  const int frbits = curve == GM_BN254 ? CurveBN254::FR_BITS : CurveBLS12377::FR_BITS;
-  if (pk->precomp) {
-    pk->preA = msm_choose_precomp(pk->nbA, frbits);
-    pk->preB = msm_choose_precomp(pk->nbB, frbits);
-    pk->preZ = msm_choose_precomp(pk->nbZ, frbits);
-    pk->preK = msm_choose_precomp(pk->nbK, frbits);
-  }
-  const size_t g1b = 2 * fp_bytes(curve), g2b = 4 * fp_bytes(curve);
-  auto up = [&](const void* src, size_t bytes, void** dst) -> int {
-    hipError_t e = hipMalloc(dst, bytes ? bytes : 16);
-    if (e != hipSuccess) {
-      set_error(std::string("pk upload hipMalloc: ") + hipGetErrorString(e));
-      return GM_ERR_OOM;
-    }
-    if (bytes) {
-      e = hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice);
-      if (e != hipSuccess) {
-        set_error(std::string("pk upload hipMemcpy: ") + hipGetErrorString(e));
-        return GM_ERR_DEVICE;
-      }
-    }
-    return GM_OK;
-  };
-  int rc;
-  // upload gnark-layout points, convert once into the device-internal layout
-  // (radix-2^29 Montgomery) the MSM kernels consume (setupDevicePointers).
-  // (with GM_PK_PRECOMPUTE also the W-1 window-shifted copies, msm_precompute_points)
-  auto up_pts = [&](const void* src, size_t count, bool g2, const MsmPrecomp& pre, void** dst) -> int {
-    void* tmp = nullptr;
-    int r = up(src, (g2 ? g2b : g1b) * count, &tmp);
-    if (r) return r;
-    size_t ib = 0;
-    if (curve == GM_BN254) ib = g2 ? msm_internal_point_bytes<CurveBN254, true>() : msm_internal_point_bytes<CurveBN254, false>();
-    else ib = g2 ? msm_internal_point_bytes<CurveBLS12377, true>() : msm_internal_point_bytes<CurveBLS12377, false>();
-    const size_t copies = pk->precomp ? pre.W : 1;
-    hipError_t e = hipMalloc(dst, ib * (count ? count * copies : 1));
-    if (e != hipSuccess) {
-      hipFree(tmp);
-      set_error(std::string("pk upload hipMalloc: ") + hipGetErrorString(e));
-      return GM_ERR_OOM;
-    }
-    if (pk->precomp) {
-      if (curve == GM_BN254)
-        r = g2 ? msm_precompute_points<CurveBN254, true>(ctx, tmp, count, pre, *dst)
-               : msm_precompute_points<CurveBN254, false>(ctx, tmp, count, pre, *dst);
-      else
-        r = g2 ? msm_precompute_points<CurveBLS12377, true>(ctx, tmp, count, pre, *dst)
-               : msm_precompute_points<CurveBLS12377, false>(ctx, tmp, count, pre, *dst);
-    } else if (curve == GM_BN254) {
-      r = g2 ? msm_prepare_points<CurveBN254, true>(ctx, tmp, count, *dst)
-             : msm_prepare_points<CurveBN254, false>(ctx, tmp, count, *dst);
-    } else {
-      r = g2 ? msm_prepare_points<CurveBLS12377, true>(ctx, tmp, count, *dst)
-             : msm_prepare_points<CurveBLS12377, false>(ctx, tmp, count, *dst);
-    }
-    hipStreamSynchronize(ctx->stream);
-    hipFree(tmp);
-    return r;
-  };
-  auto fail = [&](int code) {
-    for (void* q : {pk->A, pk->B, pk->Z, pk->K, pk->B2, pk->idxA, pk->idxB, pk->idxK})
-      if (q) hipFree(q);
-    delete pk;
-    return code;
-  };
-  // point arrays: the caller passes this shard's slice (first point = index lo)
-  if ((rc = up_pts(h->g1_A, pk->nbA, false, pk->preA, &pk->A)) ||
-      (rc = up_pts(h->g1_B, pk->nbB, false, pk->preB, &pk->B)) ||
-      (rc = up_pts(h->g1_Z, pk->nbZ, false, pk->preZ, &pk->Z)) ||
-      (rc = up_pts(h->g1_K, pk->nbK, false, pk->preK, &pk->K)) ||
-      (rc = up_pts(h->g2_B, pk->nbB, true, pk->preB, &pk->B2)))
-    return fail(rc);
-  // compaction maps (prove.go:157-178: drop wire i when InfinityA[i] / InfinityB[i])
-  std::vector<uint32_t> ia, ib, ik;
-  for (size_t i = 0; i < pk->nb_wires; i++) {
-    if (!h->infA[i]) ia.push_back((uint32_t)i);
-    if (!h->infB[i]) ib.push_back((uint32_t)i);
-  }
-  for (size_t i = 0; i < h->nbK; i++) {
-    const size_t w = h->k_wires ? (size_t)h->k_wires[i] : pk->nb_public + i;
-    if (w >= pk->nb_wires || w < pk->nb_public) {
-      set_error("pk upload: K wire index out of range");
-      return fail(GM_ERR_INVALID);
-    }
-    ik.push_back((uint32_t)w);
-  }
-  if (ia.size() != h->nbA || ib.size() != h->nbB || pk->nb_public + h->nbK > pk->nb_wires) {
-    set_error("pk upload: infinity masks inconsistent with nbA/nbB/nbK");
-    return fail(GM_ERR_INVALID);
-  }
-  // this shard's slices of the compaction maps
-  if ((rc = up(ia.data() + loA, 4 * pk->nbA, &pk->idxA)) || (rc = up(ib.data() + loB, 4 * pk->nbB, &pk->idxB)) ||
-      (rc = up(ik.data() + loK, 4 * pk->nbK, &pk->idxK)))
-    return fail(rc);
-  auto cp = [](std::vector<uint8_t>& v, const void* s, size_t b) {
-    v.resize(b);
-    memcpy(v.data(), s, b);
-  };
-  cp(pk->alpha, h->g1_alpha, g1b);
-  cp(pk->beta, h->g1_beta, g1b);
-  cp(pk->delta, h->g1_delta, g1b);
-  cp(pk->beta2, h->g2_beta, g2b);
-  cp(pk->delta2, h->g2_delta, g2b);
-  *out = pk;
-  return GM_OK;
-}
-
-int gm_g16_pk_free(gm_ctx* ctx, gm_g16_pk* pk) {
-  if (!pk) return GM_OK;
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
-  hipSetDevice(ctx->device);
-  for (void* p : {pk->A, pk->B, pk->Z, pk->K, pk->B2, pk->idxA, pk->idxB, pk->idxK})
-    if (p) hipFree(p);
-  delete pk;
-  return GM_OK;
-}
-
-extern "C++" {
-// computeH on the context's auxiliary stream, after everything already queued
-// on the main stream (the caller's a, b, c uploads).  The NTT passes overlap the
-// A, B and K MSMs, whose sorts, reductions and host round trips leave the VALUs
-// idle; wait() makes the main stream wait for h before the Z MSM.  The
-// destructor drains the auxiliary stream on every exit path.
-struct AuxComputeH {
-  gm_ctx* ctx;
-  hipEvent_t ev_in = nullptr, ev_h = nullptr;
-  explicit AuxComputeH(gm_ctx* c) : ctx(c) {}
-  template <class C>
-  int start(void* a, void* b, void* c, size_t nc, size_t n) {
-    // GM_G16_OVERLAP=0: computeH in order on the main stream (A/B measurements)
-    static const bool overlap = !getenv("GM_G16_OVERLAP") || atoi(getenv("GM_G16_OVERLAP")) != 0;
-    if (!overlap) return compute_h_device<C>(ctx, a, b, c, nc, n);
-    GM_HIP(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
-    GM_HIP(hipEventCreateWithFlags(&ev_h, hipEventDisableTiming));
-    GM_HIP(hipEventRecord(ev_in, ctx->stream));
-    GM_HIP(hipStreamWaitEvent(ctx->aux, ev_in, 0));
-    hipStream_t main = ctx->stream;
-    ctx->stream = ctx->aux;
-    int rc = compute_h_device<C>(ctx, a, b, c, nc, n);
-    ctx->stream = main;
-    if (rc) return rc;
-    GM_HIP(hipEventRecord(ev_h, ctx->aux));
-    return GM_OK;
-  }
-  int wait() {
-    if (ev_h) GM_HIP(hipStreamWaitEvent(ctx->stream, ev_h, 0));
-    return GM_OK;
-  }
-  ~AuxComputeH() {
-    hipStreamSynchronize(ctx->aux);
-    if (ev_in) hipEventDestroy(ev_in);
-    if (ev_h) hipEventDestroy(ev_h);
-  }
-};
-}  // extern "C++"
-
-extern "C++" {
-template <class C>
-static int g16_prove_t(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, void* a, void* b,
-                       void* c, size_t nc, const void* r_mont, const void* s_mont, void* ar_out,
-                       void* bs_out, void* krs_out) {
-  using HF1 = typename C::HG1F;
-  using HF2 = typename C::HG2F;
-  using HFr = typename C::HFr;
-  using J1 = host::Jac<HF1>;
-  using J2 = host::Jac<HF2>;
-  hipStream_t st = ctx->stream;
-  const size_t n = pk->n;
-  int rc;
-
-  // device-side scalar compaction (icicle.go:231-278 do this on the host + H2D)
-  Arena arena(ctx);
-  DevBuf wA, wB, wK;
-  if ((rc = wA.alloc(arena, 32 * pk->nbA)) || (rc = wB.alloc(arena, 32 * pk->nbB)) ||
-      (rc = wK.alloc(arena, 32 * pk->nbK)))
-    return rc;
-  {
-    ProfScope ps(ctx, "gather_scalars");
-    hipLaunchKernelGGL(k_gather_fr, dim3(blocks_for(pk->nbA, 256)), dim3(256), 0, st,
-                       (const uint4*)wires_dev, (const uint32_t*)pk->idxA, pk->nbA, (uint4*)wA.p);
-    hipLaunchKernelGGL(k_gather_fr, dim3(blocks_for(pk->nbB, 256)), dim3(256), 0, st,
-                       (const uint4*)wires_dev, (const uint32_t*)pk->idxB, pk->nbB, (uint4*)wB.p);
-    hipLaunchKernelGGL(k_gather_fr, dim3(blocks_for(pk->nbK, 256)), dim3(256), 0, st,
-                       (const uint4*)wires_dev, (const uint32_t*)pk->idxK, pk->nbK, (uint4*)wK.p);
-  }
-  GM_HIP(hipGetLastError());
-  // r, s, kr = -rs; deltas (icicle.go:280-295)
-  host::F<HFr> r, s;
-  memcpy(r.v, r_mont, 32);
-  memcpy(s.v, s_mont, 32);
-  host::F<HFr> kr = -(r * s);
-  host::F<HFr> rc_ = host::from_mont(r), sc_ = host::from_mont(s), krc = host::from_mont(kr);
-  host::Aff<HF1> alpha, beta, delta;
-  memcpy(&alpha, pk->alpha.data(), sizeof(alpha));
-  memcpy(&beta, pk->beta.data(), sizeof(beta));
-  memcpy(&delta, pk->delta.data(), sizeof(delta));
-  // [r]delta, [s]delta, [kr]delta (BatchScalarMultiplicationG1, prove.go:195) and
-  // [s]delta2 do not depend on the device results: computed on a host thread
-  // while the GPU runs computeH and the MSMs.
-  J1 dj = host::to_jac(delta);
-  host::Aff<HF2> beta2, delta2;
-  memcpy(&beta2, pk->beta2.data(), sizeof(beta2));
-  memcpy(&delta2, pk->delta2.data(), sizeof(delta2));
-  J1 d0, d1, d2;
-  J2 sd2;
-  std::thread deltas([&] {
-    d0 = host::jmul(dj, rc_.v, 4);
-    d1 = host::jmul(dj, sc_.v, 4);
-    d2 = host::jmul(dj, krc.v, 4);
-    sd2 = host::jmul(host::to_jac(delta2), sc_.v, 4);
-  });
-  struct Joiner {
-    std::thread& t;
-    ~Joiner() {
-      if (t.joinable()) t.join();
-    }
-  } joiner{deltas};
-  // H (computeH, icicle.go:453-513 / prove.go:356-399) -> bit-reversed h in `a`,
-  // on the auxiliary stream, overlapped with the A, B and K MSMs
-  AuxComputeH hjob(ctx);
-  if ((rc = hjob.start<C>(a, b, c, nc, n))) return rc;
-  HF1 t1[3];
-  const MsmPrecomp* pA = pk->precomp ? &pk->preA : nullptr;
-  const MsmPrecomp* pB = pk->precomp ? &pk->preB : nullptr;
-  const MsmPrecomp* pK = pk->precomp ? &pk->preK : nullptr;
-  const MsmPrecomp* pZ = pk->precomp ? &pk->preZ : nullptr;
-  // MSM results are combined below only after the delta thread has finished
-  if ((rc = msm_device<C, false>(ctx, wA.p, pk->A, pk->nbA, t1, true, pA))) return rc;
-  deltas.join();
-  // Ar = MSM(wA, A) + alpha + r delta   (computeAR1 icicle.go:312-324)
-  J1 ar = host::jadd(host::jadd_aff(J1{t1[0], t1[1], t1[2]}, alpha), d0);
-  // The G1 and G2 B-MSMs (prove.go:217,293) share scalars and layout: one
-  // sorted digit plan serves both.
-  HF2 t2[3];
-  J1 bs1;
-  {
-    Arena parena(ctx);
-    MsmPlan planB;
-    if ((rc = msm_plan<C>(ctx, parena, wB.p, pk->nbB, pB, planB))) return rc;
-    // Bs1 = MSM(wB, B) + beta + s delta   (computeBS1 icicle.go:299-310)
-    if ((rc = msm_run<C, false>(ctx, planB, pk->B, t1))) return rc;
-    bs1 = host::jadd(host::jadd_aff(J1{t1[0], t1[1], t1[2]}, beta), d1);
-    // Bs = MSM_G2(wB, B2) + s delta2 + beta2   (computeBS2 icicle.go:377-393)
-    if ((rc = msm_run<C, true>(ctx, planB, pk->B2, t2))) return rc;
-  }
-  // [s]Ar and [r]Bs1 on a host thread while the GPU runs the K and Z MSMs
-  J1 s_ar, r_bs1;
-  std::thread cross([&] {
-    s_ar = host::jmul(ar, sc_.v, 4);
-    r_bs1 = host::jmul(bs1, rc_.v, 4);
-  });
-  Joiner joiner2{cross};
-  // Krs = MSM(wK, K) + kr delta + MSM(h[:n-1], Z) + s Ar + r Bs1   (computeKRS icicle.go:326-375)
-  if ((rc = msm_device<C, false>(ctx, wK.p, pk->K, pk->nbK, t1, true, pK))) return rc;
-  J1 krs = host::jadd(J1{t1[0], t1[1], t1[2]}, d2);
-  if ((rc = hjob.wait())) return rc;
-  if ((rc = msm_device<C, false>(ctx, (char*)a + 32 * pk->zlo, pk->Z, pk->nbZ, t1, true, pZ))) return rc;
-  krs = host::jadd(krs, J1{t1[0], t1[1], t1[2]});
-  cross.join();
-  krs = host::jadd(krs, s_ar);
-  krs = host::jadd(krs, r_bs1);
-  J2 bs = host::jadd(J2{t2[0], t2[1], t2[2]}, sd2);
-  bs = host::jadd_aff(bs, beta2);
-  host::Aff<HF1> ara = host::to_aff(ar), krsa = host::to_aff(krs);
-  host::Aff<HF2> bsa = host::to_aff(bs);
-  memcpy(ar_out, &ara, sizeof(ara));
-  memcpy(krs_out, &krsa, sizeof(krsa));
-  memcpy(bs_out, &bsa, sizeof(bsa));
-  return GM_OK;
-}
-
-}  // extern "C++"
-
-int gm_g16_prove_device(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, void* a, void* b,
-                        void* c, size_t nc, const void* r, const void* s, void* ar_out,
-                        void* bs_out, void* krs_out) {
-  if (!ctx || !pk) return GM_ERR_INVALID;
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
-  GM_HIP(hipSetDevice(ctx->device));
-  int rc = pk->curve == GM_BN254
-               ? g16_prove_t<CurveBN254>(ctx, pk, wires_dev, a, b, c, nc, r, s, ar_out, bs_out, krs_out)
-               : g16_prove_t<CurveBLS12377>(ctx, pk, wires_dev, a, b, c, nc, r, s, ar_out, bs_out,
-                                            krs_out);
-  prof_collect(ctx);
-  return rc;
-}
-
-int gm_g16_prove(gm_ctx* ctx, gm_g16_pk* pk, const void* wires, const void* a, const void* b,
-                 const void* c, size_t nc, const void* r, const void* s, void* ar_out, void* bs_out,
-                 void* krs_out) {
-  if (!ctx || !pk) return GM_ERR_INVALID;
-  if (nc > pk->n) {
-    set_error("prove: more constraints than the domain size");
-    return GM_ERR_INVALID;
-  }
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
-  GM_HIP(hipSetDevice(ctx->device));
-  hipStream_t st = ctx->stream;
-  Arena arena(ctx);
-  DevBuf w, da, db, dc;
-  int rc;
-  if ((rc = w.alloc(arena, 32 * pk->nb_wires)) || (rc = da.alloc(arena, 32 * pk->n)) ||
-      (rc = db.alloc(arena, 32 * pk->n)) || (rc = dc.alloc(arena, 32 * pk->n)))
-    return rc;
-  GM_HIP(hipMemcpyAsync(w.p, wires, 32 * pk->nb_wires, hipMemcpyHostToDevice, st));
-  GM_HIP(hipMemcpyAsync(da.p, a, 32 * nc, hipMemcpyHostToDevice, st));
-  GM_HIP(hipMemcpyAsync(db.p, b, 32 * nc, hipMemcpyHostToDevice, st));
-  GM_HIP(hipMemcpyAsync(dc.p, c, 32 * nc, hipMemcpyHostToDevice, st));
-  return gm_g16_prove_device(ctx, pk, w.p, da.p, db.p, dc.p, nc, r, s, ar_out, bs_out, krs_out);
-}
-
-// ---- sharded Groth16 (BASELINE config 4) -------------------------------
-int gm_g16_partial_bytes(int curve, size_t* out) {
-  if (int rc = check_curve(curve)) return rc;
-  if (out) *out = 4 * 3 * fp_bytes(curve) + 3 * 2 * fp_bytes(curve);
-  return GM_OK;
-}
-}  // extern "C"
-
-extern "C++" {
-// The five raw MSM sums of this shard: computeH (whole domain), then the A, B,
-// K, Z (h slice) G1 MSMs and the B G2 MSM over the shard's slices.
-template <class C>
-static int g16_partial_t(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, void* a, void* b, void* c, size_t nc,
-                         uint8_t* out) {
-  using HF1 = typename C::HG1F;
-  using HF2 = typename C::HG2F;
-  hipStream_t st = ctx->stream;
-  int rc;
-  Arena arena(ctx);
-  DevBuf wA, wB, wK;
-  if ((rc = wA.alloc(arena, 32 * (pk->nbA ? pk->nbA : 1))) || (rc = wB.alloc(arena, 32 * (pk->nbB ? pk->nbB : 1))) ||
-      (rc = wK.alloc(arena, 32 * (pk->nbK ? pk->nbK : 1))))
-    return rc;
-  {
-    ProfScope ps(ctx, "gather_scalars");
-    if (pk->nbA)
-      hipLaunchKernelGGL(k_gather_fr, dim3(blocks_for(pk->nbA, 256)), dim3(256), 0, st, (const uint4*)wires_dev,
-                         (const uint32_t*)pk->idxA, pk->nbA, (uint4*)wA.p);
-    if (pk->nbB)
-      hipLaunchKernelGGL(k_gather_fr, dim3(blocks_for(pk->nbB, 256)), dim3(256), 0, st, (const uint4*)wires_dev,
-                         (const uint32_t*)pk->idxB, pk->nbB, (uint4*)wB.p);
-    if (pk->nbK)
-      hipLaunchKernelGGL(k_gather_fr, dim3(blocks_for(pk->nbK, 256)), dim3(256), 0, st, (const uint4*)wires_dev,
-                         (const uint32_t*)pk->idxK, pk->nbK, (uint4*)wK.p);
-  }
-  GM_HIP(hipGetLastError());
-  AuxComputeH hjob(ctx);
-  if ((rc = hjob.start<C>(a, b, c, nc, pk->n))) return rc;
-  const MsmPrecomp* pA = pk->precomp ? &pk->preA : nullptr;
-  const MsmPrecomp* pB = pk->precomp ? &pk->preB : nullptr;
-  const MsmPrecomp* pK = pk->precomp ? &pk->preK : nullptr;
-  const MsmPrecomp* pZ = pk->precomp ? &pk->preZ : nullptr;
-  HF1 t[3];
-  constexpr size_t J1 = sizeof(t);
-  if ((rc = msm_device<C, false>(ctx, wA.p, pk->A, pk->nbA, t, true, pA))) return rc;
-  memcpy(out, t, J1);
-  HF2 t2[3];
-  {
-    Arena parena(ctx);
-    MsmPlan planB;
-    if ((rc = msm_plan<C>(ctx, parena, wB.p, pk->nbB, pB, planB))) return rc;
-    if ((rc = msm_run<C, false>(ctx, planB, pk->B, t))) return rc;
-    memcpy(out + J1, t, J1);
-    if ((rc = msm_run<C, true>(ctx, planB, pk->B2, t2))) return rc;
-    memcpy(out + 4 * J1, t2, sizeof(t2));
-  }
-  if ((rc = msm_device<C, false>(ctx, wK.p, pk->K, pk->nbK, t, true, pK))) return rc;
-  memcpy(out + 2 * J1, t, J1);
-  if ((rc = hjob.wait())) return rc;
-  if ((rc = msm_device<C, false>(ctx, (char*)a + 32 * pk->zlo, pk->Z, pk->nbZ, t, true, pZ))) return rc;
-  memcpy(out + 3 * J1, t, J1);
-  return GM_OK;
-}
-
-// Proof elements from the summed MSMs (icicle.go:295-391 / prove.go:195-305):
-//   Ar  = sum_A + alpha + [r]delta
-//   Bs1 = sum_B + beta + [s]delta
-//   Krs = sum_K + [-rs]delta + sum_Z + [s]Ar + [r]Bs1
-//   Bs  = sum_B2 + [s]delta2 + beta2
-template <class C>
-static int g16_finish_t(const gm_g16_pk_host* h, const uint8_t* sums, const void* r_mont, const void* s_mont,
-                        void* ar_out, void* bs_out, void* krs_out) {
-  using HF1 = typename C::HG1F;
-  using HF2 = typename C::HG2F;
-  using HFr = typename C::HFr;
-  using J1 = host::Jac<HF1>;
-  using J2 = host::Jac<HF2>;
-  host::F<HFr> r, s;
-  memcpy(r.v, r_mont, 32);
-  memcpy(s.v, s_mont, 32);
-  host::F<HFr> kr = -(r * s);
-  host::F<HFr> rc_ = host::from_mont(r), sc_ = host::from_mont(s), krc = host::from_mont(kr);
-  host::Aff<HF1> alpha, beta, delta;
-  host::Aff<HF2> beta2, delta2;
-  memcpy(&alpha, h->g1_alpha, sizeof(alpha));
-  memcpy(&beta, h->g1_beta, sizeof(beta));
-  memcpy(&delta, h->g1_delta, sizeof(delta));
-  memcpy(&beta2, h->g2_beta, sizeof(beta2));
-  memcpy(&delta2, h->g2_delta, sizeof(delta2));
-  J1 sum[4];
-  J2 sum2;
-  for (int k = 0; k < 4; k++) memcpy(&sum[k], sums + k * sizeof(J1), sizeof(J1));
-  memcpy(&sum2, sums + 4 * sizeof(J1), sizeof(J2));
-  const J1 dj = host::to_jac(delta);
-  J1 ar = host::jadd(host::jadd_aff(sum[0], alpha), host::jmul(dj, rc_.v, 4));
-  J1 bs1 = host::jadd(host::jadd_aff(sum[1], beta), host::jmul(dj, sc_.v, 4));
-  J1 krs = host::jadd(sum[2], host::jmul(dj, krc.v, 4));
-  krs = host::jadd(krs, sum[3]);
-  krs = host::jadd(krs, host::jmul(ar, sc_.v, 4));
-  krs = host::jadd(krs, host::jmul(bs1, rc_.v, 4));
-  J2 bs = host::jadd(sum2, host::jmul(host::to_jac(delta2), sc_.v, 4));
-  bs = host::jadd_aff(bs, beta2);
-  host::Aff<HF1> ara = host::to_aff(ar), krsa = host::to_aff(krs);
-  host::Aff<HF2> bsa = host::to_aff(bs);
-  memcpy(ar_out, &ara, sizeof(ara));
-  memcpy(krs_out, &krsa, sizeof(krsa));
-  memcpy(bs_out, &bsa, sizeof(bsa));
-  return GM_OK;
-}
-}  // extern "C++"
-
-extern "C" {
-int gm_g16_prove_partial(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, void* a_dev, void* b_dev, void* c_dev,
-                         size_t nc, void* partial_out) {
-  if (!ctx || !pk || !partial_out) return GM_ERR_INVALID;
-  if (nc > pk->n) {
-    set_error("prove: more constraints than the domain size");
-    return GM_ERR_INVALID;
-  }
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
-  GM_HIP(hipSetDevice(ctx->device));
-  int rc = pk->curve == GM_BN254
-               ? g16_partial_t<CurveBN254>(ctx, pk, wires_dev, a_dev, b_dev, c_dev, nc, (uint8_t*)partial_out)
-               : g16_partial_t<CurveBLS12377>(ctx, pk, wires_dev, a_dev, b_dev, c_dev, nc, (uint8_t*)partial_out);
-  prof_collect(ctx);
-  return rc;
-}
-
-int gm_g16_finish(int curve, const gm_g16_pk_host* h, const void* sums, const void* r, const void* s, void* ar_out,
-                  void* bs_out, void* krs_out) {
-  if (int rc = check_curve(curve)) return rc;
-  if (!h || !sums || !r || !s || !ar_out || !bs_out || !krs_out) return GM_ERR_INVALID;
-  return curve == GM_BN254
-             ? g16_finish_t<CurveBN254>(h, (const uint8_t*)sums, r, s, ar_out, bs_out, krs_out)
-             : g16_finish_t<CurveBLS12377>(h, (const uint8_t*)sums, r, s, ar_out, bs_out, krs_out);
-}
 }  // extern "C"

@@ -1,0 +1,1030 @@
+// Groth16 prover on one or several MI355X GPUs -- replaces the device block of
+// icicle_bn254.Prove (backend/groth16/bn254/icicle/icicle.go:133-422),
+// re-derived from the current CPU prover groth16_bn254.Prove
+// (backend/groth16/bn254/prove.go:62-325) as SURVEY.md §0.3 prescribes: only
+// computeH, the compaction and the five MSMs move to the device; the O(1)
+// finishing adds (prove.go:195-305) run on the host.
+//
+// One proof = five MSM sums over the key's (sharded) point arrays:
+//   A  = <wA, pk.G1.A>,  B = <wB, pk.G1.B>,  B2 = <wB, pk.G2.B>,
+//   K  = <wK, pk.G1.K>,  Z = <h[:n-1], pk.G1.Z>
+// g16_sums_t computes them on one device; an HSource supplies h (computeH on
+// this device from resident or host-staged a/b/c, or slices distributed by
+// another device of a gm_multi).  Sums of several shards / devices add up.
+#include <atomic>
+#include <cstdint>
+#include <condition_variable>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "curves.hpp"
+#include "msm.hpp"
+#include "ntt.hpp"
+#include "runtime.hpp"
+
+using namespace gm;
+
+struct gm_g16_pk {
+  int curve;
+  size_t n, nb_wires, nb_public, nbA, nbB, nbK;
+  void *A = nullptr, *B = nullptr, *Z = nullptr, *K = nullptr, *B2 = nullptr;  // device point arrays
+  void *idxA = nullptr, *idxB = nullptr, *idxK = nullptr;  // device compaction maps (wire - wlo)
+  size_t zlo = 0, nbZ = 0;      // this key's slice of h / pk.G1.Z (whole key: 0, n-1)
+  size_t wlo = 0, whi = 0;      // wires the maps address: [wlo, whi) (whole key: 0, nb_wires)
+  bool precomp = false;         // GM_PK_PRECOMPUTE: fixed-base window copies
+  MsmPrecomp preA, preB, preZ, preK;  // layouts (B and B2 share preB)
+  std::vector<uint8_t> alpha, beta, delta, beta2, delta2;  // host affine
+};
+
+namespace gm {
+namespace {
+
+int check_curve_id(int curve) {
+  if (curve != GM_BN254 && curve != GM_BLS12_377) {
+    set_error("unknown curve id");
+    return GM_ERR_INVALID;
+  }
+  return GM_OK;
+}
+
+// dst[i] = src[idx[i]] (Fr, 32 bytes) -- device-side scalar compaction
+__global__ void k_gather_fr(const uint4* __restrict__ src, const uint32_t* __restrict__ idx, size_t n,
+                            uint4* __restrict__ dst) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const size_t j = idx[i];
+  dst[2 * i] = src[2 * j];
+  dst[2 * i + 1] = src[2 * j + 1];
+}
+
+// [lo, hi) of rank's contiguous shard of n items (gnark_mi355x.shard_range)
+void shard_of(size_t n, int rank, int world, size_t* lo, size_t* hi) {
+  const size_t q = n / (size_t)world, r = n % (size_t)world;
+  *lo = (size_t)rank * q + std::min((size_t)rank, r);
+  *hi = *lo + q + ((size_t)rank < r ? 1 : 0);
+}
+
+// [lo, hi) of part k of n items split in proportion to weights w
+void shard_weighted(size_t n, const std::vector<double>& w, int k, size_t* lo, size_t* hi) {
+  double tot = 0, before = 0;
+  for (size_t i = 0; i < w.size(); i++) {
+    tot += w[i];
+    if ((int)i < k) before += w[i];
+  }
+  *lo = (size_t)((double)n * before / tot);
+  *hi = k + 1 == (int)w.size() ? n : (size_t)((double)n * (before + w[k]) / tot);
+}
+
+struct Ranges {
+  size_t loA, hiA, loB, hiB, loK, hiK, loZ, hiZ;
+  bool rebase;  // index maps relative to the lowest wire they address (gm_multi keys)
+};
+
+size_t internal_point_bytes(int curve, bool g2) {
+  if (curve == GM_BN254)
+    return g2 ? msm_internal_point_bytes<CurveBN254, true>() : msm_internal_point_bytes<CurveBN254, false>();
+  return g2 ? msm_internal_point_bytes<CurveBLS12377, true>() : msm_internal_point_bytes<CurveBLS12377, false>();
+}
+
+void pk_release(gm_g16_pk* pk) {
+  for (void* q : {pk->A, pk->B, pk->Z, pk->K, pk->B2, pk->idxA, pk->idxB, pk->idxK})
+    if (q) hipFree(q);
+  delete pk;
+}
+
+// Uploads the [lo, hi) slices of the key's point arrays (h's pointers address
+// the first point of each slice) and the matching slices of the compaction maps
+// (setupDevicePointers, icicle.go:31-130; the maps replace icicle.go:231-278's
+// host filtering, prove.go:157-178 / 243-245).
+int pk_upload_ranges(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsigned flags, const Ranges& rg,
+                     gm_g16_pk** out) {
+  auto* pk = new gm_g16_pk();
+  pk->curve = curve;
+  pk->n = h->domain_size;
+  pk->nb_wires = h->nb_wires;
+  pk->nb_public = h->nb_public;
+  pk->nbA = rg.hiA - rg.loA;
+  pk->nbB = rg.hiB - rg.loB;
+  pk->nbK = rg.hiK - rg.loK;
+  pk->zlo = rg.loZ;
+  pk->nbZ = rg.hiZ - rg.loZ;
+  pk->precomp = (flags & GM_PK_PRECOMPUTE) != 0;
+  const int frbits = curve == GM_BN254 ? CurveBN254::FR_BITS : CurveBLS12377::FR_BITS;
+  if (pk->precomp) {
+    pk->preA = msm_choose_precomp(pk->nbA, frbits);
+    pk->preB = msm_choose_precomp(pk->nbB, frbits);
+    pk->preZ = msm_choose_precomp(pk->nbZ, frbits);
+    pk->preK = msm_choose_precomp(pk->nbK, frbits);
+  }
+  const size_t g1b = 2 * fp_bytes(curve), g2b = 4 * fp_bytes(curve);
+  auto fail = [&](int code) {
+    pk_release(pk);
+    return code;
+  };
+  auto up = [&](const void* src, size_t bytes, void** dst) -> int {
+    hipError_t e = hipMalloc(dst, bytes ? bytes : 16);
+    if (e != hipSuccess) {
+      set_error(std::string("pk upload hipMalloc: ") + hipGetErrorString(e));
+      return GM_ERR_OOM;
+    }
+    if (bytes) {
+      e = hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice);
+      if (e != hipSuccess) {
+        set_error(std::string("pk upload hipMemcpy: ") + hipGetErrorString(e));
+        return GM_ERR_DEVICE;
+      }
+    }
+    return GM_OK;
+  };
+  // gnark-layout points -> device-internal layout, once (plus the W-1
+  // window-shifted copies with GM_PK_PRECOMPUTE, msm_precompute_points)
+  auto up_pts = [&](const void* src, size_t count, bool g2, const MsmPrecomp& pre, void** dst) -> int {
+    void* tmp = nullptr;
+    int r = up(src, (g2 ? g2b : g1b) * count, &tmp);
+    if (r) {
+      if (tmp) hipFree(tmp);
+      return r;
+    }
+    const size_t copies = pk->precomp ? pre.W : 1;
+    hipError_t e = hipMalloc(dst, internal_point_bytes(curve, g2) * (count ? count * copies : 1));
+    if (e != hipSuccess) {
+      hipFree(tmp);
+      set_error(std::string("pk upload hipMalloc: ") + hipGetErrorString(e));
+      return GM_ERR_OOM;
+    }
+    if (pk->precomp) {
+      if (curve == GM_BN254)
+        r = g2 ? msm_precompute_points<CurveBN254, true>(ctx, tmp, count, pre, *dst)
+               : msm_precompute_points<CurveBN254, false>(ctx, tmp, count, pre, *dst);
+      else
+        r = g2 ? msm_precompute_points<CurveBLS12377, true>(ctx, tmp, count, pre, *dst)
+               : msm_precompute_points<CurveBLS12377, false>(ctx, tmp, count, pre, *dst);
+    } else if (curve == GM_BN254) {
+      r = g2 ? msm_prepare_points<CurveBN254, true>(ctx, tmp, count, *dst)
+             : msm_prepare_points<CurveBN254, false>(ctx, tmp, count, *dst);
+    } else {
+      r = g2 ? msm_prepare_points<CurveBLS12377, true>(ctx, tmp, count, *dst)
+             : msm_prepare_points<CurveBLS12377, false>(ctx, tmp, count, *dst);
+    }
+    hipStreamSynchronize(ctx->stream);
+    hipFree(tmp);
+    return r;
+  };
+  int rc;
+  if ((rc = up_pts(h->g1_A, pk->nbA, false, pk->preA, &pk->A)) ||
+      (rc = up_pts(h->g1_B, pk->nbB, false, pk->preB, &pk->B)) ||
+      (rc = up_pts(h->g1_Z, pk->nbZ, false, pk->preZ, &pk->Z)) ||
+      (rc = up_pts(h->g1_K, pk->nbK, false, pk->preK, &pk->K)) ||
+      (rc = up_pts(h->g2_B, pk->nbB, true, pk->preB, &pk->B2)))
+    return fail(rc);
+  // compaction maps (prove.go:157-178: drop wire i when InfinityA[i] / InfinityB[i];
+  // K: the k_wires survivors of filterHeap, prove.go:243-245, or nb_public + i)
+  std::vector<uint32_t> ia, ib, ik;
+  for (size_t i = 0; i < pk->nb_wires; i++) {
+    if (!h->infA[i]) ia.push_back((uint32_t)i);
+    if (!h->infB[i]) ib.push_back((uint32_t)i);
+  }
+  for (size_t i = 0; i < h->nbK; i++) {
+    const size_t w = h->k_wires ? (size_t)h->k_wires[i] : pk->nb_public + i;
+    if (w >= pk->nb_wires || w < pk->nb_public) {
+      set_error("pk upload: K wire index out of range");
+      return fail(GM_ERR_INVALID);
+    }
+    ik.push_back((uint32_t)w);
+  }
+  if (ia.size() != h->nbA || ib.size() != h->nbB || pk->nb_public + h->nbK > pk->nb_wires) {
+    set_error("pk upload: infinity masks inconsistent with nbA/nbB/nbK");
+    return fail(GM_ERR_INVALID);
+  }
+  // wire range this key's slices read
+  pk->wlo = 0;
+  pk->whi = pk->nb_wires;
+  if (rg.rebase) {
+    size_t lo = SIZE_MAX, hi = 0;
+    auto span = [&](const std::vector<uint32_t>& v, size_t a, size_t b) {
+      for (size_t i = a; i < b; i++) {
+        lo = std::min(lo, (size_t)v[i]);
+        hi = std::max(hi, (size_t)v[i] + 1);
+      }
+    };
+    span(ia, rg.loA, rg.hiA);
+    span(ib, rg.loB, rg.hiB);
+    span(ik, rg.loK, rg.hiK);
+    if (hi <= lo) lo = hi = 0;
+    pk->wlo = lo;
+    pk->whi = hi;
+    for (auto* v : {&ia, &ib, &ik})
+      for (auto& x : *v) x -= (x >= lo ? (uint32_t)lo : x);  // entries outside the slice are never read
+  }
+  if ((rc = up(ia.data() + rg.loA, 4 * pk->nbA, &pk->idxA)) || (rc = up(ib.data() + rg.loB, 4 * pk->nbB, &pk->idxB)) ||
+      (rc = up(ik.data() + rg.loK, 4 * pk->nbK, &pk->idxK)))
+    return fail(rc);
+  auto cp = [](std::vector<uint8_t>& v, const void* s, size_t b) {
+    v.resize(b);
+    memcpy(v.data(), s, b);
+  };
+  cp(pk->alpha, h->g1_alpha, g1b);
+  cp(pk->beta, h->g1_beta, g1b);
+  cp(pk->delta, h->g1_delta, g1b);
+  cp(pk->beta2, h->g2_beta, g2b);
+  cp(pk->delta2, h->g2_delta, g2b);
+  *out = pk;
+  return GM_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Sources of h (the bit-reversed computeH output, icicle.go:453-513 /
+// prove.go:356-399) for the Z MSM.  poll() is called between the A/B/K MSMs
+// (which need no h) and launches work whose inputs have arrived; z_scalars()
+// makes the main stream wait for this key's slice of h and returns it.
+// ---------------------------------------------------------------------------
+struct HSource {
+  virtual ~HSource() {}
+  virtual int poll() { return GM_OK; }
+  virtual int z_scalars(const void** zs) = 0;
+};
+
+// computeH on the context's auxiliary stream, overlapped with the MSMs (whose
+// sorts, reductions and host round trips leave the VALUs idle).
+// GM_G16_OVERLAP=0 runs it in order on the main stream (A/B measurements).
+template <class C>
+int launch_compute_h(gm_ctx* ctx, void* a, void* b, void* c, size_t nc, size_t n, hipEvent_t wait_for,
+                     hipEvent_t done) {
+  static const bool overlap = !getenv("GM_G16_OVERLAP") || atoi(getenv("GM_G16_OVERLAP")) != 0;
+  if (!overlap) {
+    if (wait_for) GM_HIP(hipStreamWaitEvent(ctx->stream, wait_for, 0));
+    int rc = compute_h_device<C>(ctx, a, b, c, nc, n);
+    if (rc) return rc;
+    GM_HIP(hipEventRecord(done, ctx->stream));
+    return GM_OK;
+  }
+  if (wait_for) GM_HIP(hipStreamWaitEvent(ctx->aux, wait_for, 0));
+  hipStream_t main = ctx->stream;
+  ctx->stream = ctx->aux;
+  int rc = compute_h_device<C>(ctx, a, b, c, nc, n);
+  ctx->stream = main;
+  if (rc) return rc;
+  GM_HIP(hipEventRecord(done, ctx->aux));
+  return GM_OK;
+}
+
+struct EventPair {
+  hipEvent_t a = nullptr, b = nullptr;
+  int create() {
+    GM_HIP(hipEventCreateWithFlags(&a, hipEventDisableTiming));
+    GM_HIP(hipEventCreateWithFlags(&b, hipEventDisableTiming));
+    return GM_OK;
+  }
+  ~EventPair() {
+    if (a) hipEventDestroy(a);
+    if (b) hipEventDestroy(b);
+  }
+};
+
+// a, b, c already on the device (queued on the main stream): computeH starts at once.
+template <class C>
+struct DeviceH : HSource {
+  gm_ctx* ctx;
+  gm_g16_pk* pk;
+  void *a, *b, *c;
+  size_t nc;
+  EventPair ev;  // a: inputs ready (main stream), b: h ready
+  DeviceH(gm_ctx* x, gm_g16_pk* k, void* a_, void* b_, void* c_, size_t n_) : ctx(x), pk(k), a(a_), b(b_), c(c_), nc(n_) {}
+  int start() {
+    int rc;
+    if ((rc = ev.create())) return rc;
+    GM_HIP(hipEventRecord(ev.a, ctx->stream));
+    return launch_compute_h<C>(ctx, a, b, c, nc, pk->n, ev.a, ev.b);
+  }
+  int z_scalars(const void** zs) override {
+    GM_HIP(hipStreamWaitEvent(ctx->stream, ev.b, 0));
+    *zs = (const char*)a + 32 * pk->zlo;
+    return GM_OK;
+  }
+  ~DeviceH() override { hipStreamSynchronize(ctx->aux); }
+};
+
+// a, b, c in host memory: a helper thread copies them on the context's copy
+// stream (pageable hipMemcpyAsync runs at ~56 GB/s on the box but blocks the
+// calling thread) while the main thread runs the A/B/K MSMs; computeH is
+// launched on the auxiliary stream at the first poll() after the copies are
+// queued.  `after_h` (multi-device) runs right after the launch.
+template <class C>
+struct HostStagedH : HSource {
+  gm_ctx* ctx;
+  gm_g16_pk* pk;
+  void *da, *db, *dc;
+  const void *ha, *hb, *hc;
+  size_t nc;
+  EventPair ev;  // a: copies done (copy stream), b: h ready
+  std::thread th;
+  std::atomic<bool> queued{false};
+  std::atomic<int> copy_rc{GM_OK};
+  std::string copy_err;
+  bool launched = false;
+  std::function<int()> after_h;
+  HostStagedH(gm_ctx* x, gm_g16_pk* k, void* a_, void* b_, void* c_, const void* ha_, const void* hb_,
+              const void* hc_, size_t n_)
+      : ctx(x), pk(k), da(a_), db(b_), dc(c_), ha(ha_), hb(hb_), hc(hc_), nc(n_) {}
+  int start() {
+    int rc;
+    if ((rc = ev.create())) return rc;
+    th = std::thread([this] {
+      int r = GM_OK;
+      if (hipSetDevice(ctx->device) != hipSuccess) r = GM_ERR_DEVICE;
+      const void* src[3] = {ha, hb, hc};
+      void* dst[3] = {da, db, dc};
+      for (int k = 0; k < 3 && r == GM_OK; k++)
+        if (nc && hipMemcpyAsync(dst[k], src[k], 32 * nc, hipMemcpyHostToDevice, ctx->copy) != hipSuccess)
+          r = GM_ERR_DEVICE;
+      if (r == GM_OK && hipEventRecord(ev.a, ctx->copy) != hipSuccess) r = GM_ERR_DEVICE;
+      if (r) copy_err = "staged a/b/c upload failed";
+      copy_rc = r;
+      queued = true;
+    });
+    return GM_OK;
+  }
+  int launch(bool block) {
+    if (launched) return GM_OK;
+    if (!block && !queued.load()) return GM_OK;
+    if (th.joinable()) th.join();
+    if (copy_rc) {
+      set_error(copy_err);
+      return copy_rc;
+    }
+    launched = true;
+    int rc = launch_compute_h<C>(ctx, da, db, dc, nc, pk->n, ev.a, ev.b);
+    if (rc) return rc;
+    return after_h ? after_h() : GM_OK;
+  }
+  int poll() override { return launch(false); }
+  int z_scalars(const void** zs) override {
+    int rc;
+    if ((rc = launch(true))) return rc;
+    GM_HIP(hipStreamWaitEvent(ctx->stream, ev.b, 0));
+    *zs = (const char*)da + 32 * pk->zlo;
+    return GM_OK;
+  }
+  ~HostStagedH() override {
+    if (th.joinable()) th.join();
+    hipStreamSynchronize(ctx->copy);
+    hipStreamSynchronize(ctx->aux);
+  }
+};
+
+// h slice delivered by another device (gm_multi): wait until the producer has
+// queued the peer copy into `dst`, then for that copy itself.
+struct SharedH {
+  std::mutex mu;
+  std::condition_variable cv;
+  bool ready = false;
+  int rc = GM_OK;
+  hipEvent_t done = nullptr;  // on the producer's auxiliary stream, after the peer copies
+};
+struct RemoteH : HSource {
+  SharedH* sh;
+  const void* dst;
+  RemoteH(SharedH* s, const void* d) : sh(s), dst(d) {}
+  int z_scalars(const void** zs) override {
+    std::unique_lock<std::mutex> lk(sh->mu);
+    sh->cv.wait(lk, [&] { return sh->ready; });
+    if (sh->rc) {
+      set_error("h producer device failed");
+      return sh->rc;
+    }
+    GM_HIP(hipEventSynchronize(sh->done));
+    *zs = dst;
+    return GM_OK;
+  }
+};
+
+template <class C>
+struct G16Sums {
+  typename C::HG1F A[3], B[3], K[3], Z[3];
+  typename C::HG2F B2[3];
+};
+
+// The five MSM sums of one key (slice) on one device.  on_ab(A, B) runs on the
+// host as soon as A and B are known (the prover starts the cross terms then).
+template <class C>
+int g16_sums_t(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, HSource& hs, G16Sums<C>& out,
+               const std::function<void(const G16Sums<C>&)>& on_ab) {
+  hipStream_t st = ctx->stream;
+  int rc;
+  Arena arena(ctx);
+  DevBuf wA, wB, wK;
+  if ((rc = wA.alloc(arena, 32 * (pk->nbA ? pk->nbA : 1))) || (rc = wB.alloc(arena, 32 * (pk->nbB ? pk->nbB : 1))) ||
+      (rc = wK.alloc(arena, 32 * (pk->nbK ? pk->nbK : 1))))
+    return rc;
+  {
+    // device-side scalar compaction (icicle.go:231-278 do this on the host + H2D)
+    ProfScope ps(ctx, "gather_scalars");
+    if (pk->nbA)
+      hipLaunchKernelGGL(k_gather_fr, dim3(blocks_for(pk->nbA, 256)), dim3(256), 0, st, (const uint4*)wires_dev,
+                         (const uint32_t*)pk->idxA, pk->nbA, (uint4*)wA.p);
+    if (pk->nbB)
+      hipLaunchKernelGGL(k_gather_fr, dim3(blocks_for(pk->nbB, 256)), dim3(256), 0, st, (const uint4*)wires_dev,
+                         (const uint32_t*)pk->idxB, pk->nbB, (uint4*)wB.p);
+    if (pk->nbK)
+      hipLaunchKernelGGL(k_gather_fr, dim3(blocks_for(pk->nbK, 256)), dim3(256), 0, st, (const uint4*)wires_dev,
+                         (const uint32_t*)pk->idxK, pk->nbK, (uint4*)wK.p);
+  }
+  GM_HIP(hipGetLastError());
+  const MsmPrecomp* pA = pk->precomp ? &pk->preA : nullptr;
+  const MsmPrecomp* pB = pk->precomp ? &pk->preB : nullptr;
+  const MsmPrecomp* pK = pk->precomp ? &pk->preK : nullptr;
+  const MsmPrecomp* pZ = pk->precomp ? &pk->preZ : nullptr;
+  if ((rc = hs.poll())) return rc;
+  if ((rc = msm_device<C, false>(ctx, wA.p, pk->A, pk->nbA, out.A, true, pA))) return rc;
+  if ((rc = hs.poll())) return rc;
+  {
+    // the G1 and G2 B-MSMs (prove.go:217,293) share scalars and layout: one plan
+    Arena parena(ctx);
+    MsmPlan planB;
+    if ((rc = msm_plan<C>(ctx, parena, wB.p, pk->nbB, pB, planB))) return rc;
+    if ((rc = msm_run<C, false>(ctx, planB, pk->B, out.B))) return rc;
+    if (on_ab) on_ab(out);
+    if ((rc = hs.poll())) return rc;
+    if ((rc = msm_run<C, true>(ctx, planB, pk->B2, out.B2))) return rc;
+  }
+  if ((rc = hs.poll())) return rc;
+  if ((rc = msm_device<C, false>(ctx, wK.p, pk->K, pk->nbK, out.K, true, pK))) return rc;
+  const void* zs = nullptr;
+  if ((rc = hs.z_scalars(&zs))) return rc;
+  return msm_device<C, false>(ctx, zs, pk->Z, pk->nbZ, out.Z, true, pZ);
+}
+
+// Host finishing of icicle.go:280-391 / prove.go:183-305 from the raw sums:
+//   Ar  = A + alpha + [r]delta
+//   Bs1 = B + beta + [s]delta
+//   Krs = K + [-rs]delta + Z + [s]Ar + [r]Bs1
+//   Bs  = B2 + [s]delta2 + beta2
+// The four scalar multiplications that do not depend on the device results run
+// on a host thread started before the MSMs (begin()); [s]Ar and [r]Bs1 on a
+// second one as soon as A and B are known (cross()).
+template <class C>
+struct G16Finish {
+  using HF1 = typename C::HG1F;
+  using HF2 = typename C::HG2F;
+  using HFr = typename C::HFr;
+  using J1 = host::Jac<HF1>;
+  using J2 = host::Jac<HF2>;
+  host::Aff<HF1> alpha, beta, delta;
+  host::Aff<HF2> beta2, delta2;
+  host::F<HFr> rc_, sc_, krc;
+  J1 d0, d1, d2, ar, bs1, s_ar, r_bs1;
+  J2 sd2;
+  std::thread t_deltas, t_cross;
+
+  G16Finish(const uint8_t* alpha_, const uint8_t* beta_, const uint8_t* delta_, const uint8_t* beta2_,
+            const uint8_t* delta2_, const void* r_mont, const void* s_mont) {
+    memcpy(&alpha, alpha_, sizeof(alpha));
+    memcpy(&beta, beta_, sizeof(beta));
+    memcpy(&delta, delta_, sizeof(delta));
+    memcpy(&beta2, beta2_, sizeof(beta2));
+    memcpy(&delta2, delta2_, sizeof(delta2));
+    host::F<HFr> r, s;
+    memcpy(r.v, r_mont, 32);
+    memcpy(s.v, s_mont, 32);
+    const host::F<HFr> kr = -(r * s);  // _kr = -(r s) (prove.go:189)
+    rc_ = host::from_mont(r);
+    sc_ = host::from_mont(s);
+    krc = host::from_mont(kr);
+  }
+  // [r]delta, [s]delta, [kr]delta (BatchScalarMultiplicationG1, prove.go:195), [s]delta2
+  void begin() {
+    t_deltas = std::thread([this] {
+      const J1 dj = host::to_jac(delta);
+      d0 = host::jmul(dj, rc_.v, 4);
+      d1 = host::jmul(dj, sc_.v, 4);
+      d2 = host::jmul(dj, krc.v, 4);
+      sd2 = host::jmul(host::to_jac(delta2), sc_.v, 4);
+    });
+  }
+  void cross(const HF1 (&A)[3], const HF1 (&B)[3]) {
+    if (t_deltas.joinable()) t_deltas.join();
+    ar = host::jadd(host::jadd_aff(J1{A[0], A[1], A[2]}, alpha), d0);
+    bs1 = host::jadd(host::jadd_aff(J1{B[0], B[1], B[2]}, beta), d1);
+    t_cross = std::thread([this] {
+      s_ar = host::jmul(ar, sc_.v, 4);
+      r_bs1 = host::jmul(bs1, rc_.v, 4);
+    });
+  }
+  void join() {
+    if (t_deltas.joinable()) t_deltas.join();
+    if (t_cross.joinable()) t_cross.join();
+  }
+  void finish(const G16Sums<C>& s, void* ar_out, void* bs_out, void* krs_out) {
+    if (!t_cross.joinable() && !crossed) cross(s.A, s.B);
+    join();
+    J1 krs = host::jadd(J1{s.K[0], s.K[1], s.K[2]}, d2);
+    krs = host::jadd(krs, J1{s.Z[0], s.Z[1], s.Z[2]});
+    krs = host::jadd(krs, s_ar);
+    krs = host::jadd(krs, r_bs1);
+    J2 bs = host::jadd(J2{s.B2[0], s.B2[1], s.B2[2]}, sd2);
+    bs = host::jadd_aff(bs, beta2);
+    const host::Aff<HF1> ara = host::to_aff(ar), krsa = host::to_aff(krs);
+    const host::Aff<HF2> bsa = host::to_aff(bs);
+    memcpy(ar_out, &ara, sizeof(ara));
+    memcpy(krs_out, &krsa, sizeof(krsa));
+    memcpy(bs_out, &bsa, sizeof(bsa));
+  }
+  bool crossed = false;
+  ~G16Finish() { join(); }
+};
+
+template <class C>
+G16Finish<C>* make_finish(const gm_g16_pk* pk, const void* r, const void* s) {
+  return new G16Finish<C>(pk->alpha.data(), pk->beta.data(), pk->delta.data(), pk->beta2.data(), pk->delta2.data(),
+                          r, s);
+}
+
+// One device, whole key.  host_abc: a, b, c are host pointers staged on the copy
+// stream; else device buffers (queued on the main stream).
+template <class C>
+int g16_prove_t(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, void* a, void* b, void* c, const void* ha,
+                const void* hb, const void* hc, size_t nc, const void* r, const void* s, void* ar_out, void* bs_out,
+                void* krs_out) {
+  std::unique_ptr<G16Finish<C>> fin(make_finish<C>(pk, r, s));
+  fin->begin();
+  std::unique_ptr<HSource> hs;
+  int rc;
+  if (ha) {
+    auto* x = new HostStagedH<C>(ctx, pk, a, b, c, ha, hb, hc, nc);
+    hs.reset(x);
+    rc = x->start();
+  } else {
+    auto* x = new DeviceH<C>(ctx, pk, a, b, c, nc);
+    hs.reset(x);
+    rc = x->start();
+  }
+  if (rc) return rc;
+  G16Sums<C> sums;
+  auto on_ab = [&](const G16Sums<C>& sm) {
+    fin->cross(sm.A, sm.B);
+    fin->crossed = true;
+  };
+  if ((rc = g16_sums_t<C>(ctx, pk, wires_dev, *hs, sums, on_ab))) return rc;
+  fin->finish(sums, ar_out, bs_out, krs_out);
+  return GM_OK;
+}
+
+template <class C>
+void sums_to_bytes(const G16Sums<C>& s, uint8_t* out) {
+  constexpr size_t J1 = sizeof(s.A);
+  memcpy(out, s.A, J1);
+  memcpy(out + J1, s.B, J1);
+  memcpy(out + 2 * J1, s.K, J1);
+  memcpy(out + 3 * J1, s.Z, J1);
+  memcpy(out + 4 * J1, s.B2, sizeof(s.B2));
+}
+template <class C>
+void bytes_to_sums(const uint8_t* in, G16Sums<C>& s) {
+  constexpr size_t J1 = sizeof(s.A);
+  memcpy(s.A, in, J1);
+  memcpy(s.B, in + J1, J1);
+  memcpy(s.K, in + 2 * J1, J1);
+  memcpy(s.Z, in + 3 * J1, J1);
+  memcpy(s.B2, in + 4 * J1, sizeof(s.B2));
+}
+template <class C>
+void add_sums(G16Sums<C>& acc, const G16Sums<C>& x) {
+  using J1 = host::Jac<typename C::HG1F>;
+  using J2 = host::Jac<typename C::HG2F>;
+  auto add1 = [](typename C::HG1F (&a)[3], const typename C::HG1F (&b)[3]) {
+    const J1 r = host::jadd(J1{a[0], a[1], a[2]}, J1{b[0], b[1], b[2]});
+    a[0] = r.x;
+    a[1] = r.y;
+    a[2] = r.z;
+  };
+  add1(acc.A, x.A);
+  add1(acc.B, x.B);
+  add1(acc.K, x.K);
+  add1(acc.Z, x.Z);
+  const J2 r = host::jadd(J2{acc.B2[0], acc.B2[1], acc.B2[2]}, J2{x.B2[0], x.B2[1], x.B2[2]});
+  acc.B2[0] = r.x;
+  acc.B2[1] = r.y;
+  acc.B2[2] = r.z;
+}
+
+}  // namespace
+}  // namespace gm
+
+// ===========================================================================
+// single-device C-ABI
+// ===========================================================================
+extern "C" {
+
+int gm_g16_pk_upload(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, gm_g16_pk** out) {
+  return gm_g16_pk_upload_ex(ctx, curve, h, 0u, out);
+}
+
+int gm_g16_pk_upload_ex(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsigned flags, gm_g16_pk** out) {
+  return gm_g16_pk_upload_shard(ctx, curve, h, flags, 0, 1, out);
+}
+
+int gm_g16_pk_upload_shard(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsigned flags, int rank, int world,
+                           gm_g16_pk** out) {
+  if (int rc = check_curve_id(curve)) return rc;
+  if (flags & ~(unsigned)GM_PK_PRECOMPUTE) {
+    set_error("pk upload: unknown flags");
+    return GM_ERR_INVALID;
+  }
+  if (!ctx || !h || !out || h->domain_size < 2) return GM_ERR_INVALID;
+  if (world < 1 || rank < 0 || rank >= world) {
+    set_error("pk upload: bad rank / world");
+    return GM_ERR_INVALID;
+  }
+  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  GM_HIP(hipSetDevice(ctx->device));
+  Ranges rg;
+  shard_of(h->nbA, rank, world, &rg.loA, &rg.hiA);
+  shard_of(h->nbB, rank, world, &rg.loB, &rg.hiB);
+  shard_of(h->nbK, rank, world, &rg.loK, &rg.hiK);
+  shard_of(h->domain_size - 1, rank, world, &rg.loZ, &rg.hiZ);
+  rg.rebase = false;
+  return pk_upload_ranges(ctx, curve, h, flags, rg, out);
+}
+
+int gm_g16_pk_free(gm_ctx* ctx, gm_g16_pk* pk) {
+  if (!pk) return GM_OK;
+  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  hipSetDevice(ctx->device);
+  pk_release(pk);
+  return GM_OK;
+}
+
+int gm_g16_prove_device(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, void* a, void* b, void* c, size_t nc,
+                        const void* r, const void* s, void* ar_out, void* bs_out, void* krs_out) {
+  if (!ctx || !pk || !r || !s || !ar_out || !bs_out || !krs_out) return GM_ERR_INVALID;
+  if (nc > pk->n) {
+    set_error("prove: more constraints than the domain size");
+    return GM_ERR_INVALID;
+  }
+  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  GM_HIP(hipSetDevice(ctx->device));
+  int rc = pk->curve == GM_BN254 ? g16_prove_t<CurveBN254>(ctx, pk, wires_dev, a, b, c, nullptr, nullptr, nullptr,
+                                                           nc, r, s, ar_out, bs_out, krs_out)
+                                 : g16_prove_t<CurveBLS12377>(ctx, pk, wires_dev, a, b, c, nullptr, nullptr, nullptr,
+                                                              nc, r, s, ar_out, bs_out, krs_out);
+  prof_collect(ctx);
+  return rc;
+}
+
+// Host inputs (the icicle.go:204-412 scope, H2D included): the wires are
+// copied first (every MSM needs them), a / b / c on the copy stream by a helper
+// thread while the A/B/K MSMs run.
+int gm_g16_prove(gm_ctx* ctx, gm_g16_pk* pk, const void* wires, const void* a, const void* b, const void* c,
+                 size_t nc, const void* r, const void* s, void* ar_out, void* bs_out, void* krs_out) {
+  if (!ctx || !pk || !wires || !a || !b || !c || !r || !s || !ar_out || !bs_out || !krs_out) return GM_ERR_INVALID;
+  if (nc > pk->n) {
+    set_error("prove: more constraints than the domain size");
+    return GM_ERR_INVALID;
+  }
+  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  GM_HIP(hipSetDevice(ctx->device));
+  Arena arena(ctx);
+  DevBuf w, da, db, dc;
+  int rc;
+  if ((rc = w.alloc(arena, 32 * pk->nb_wires)) || (rc = da.alloc(arena, 32 * pk->n)) ||
+      (rc = db.alloc(arena, 32 * pk->n)) || (rc = dc.alloc(arena, 32 * pk->n)))
+    return rc;
+  GM_HIP(hipMemcpyAsync(w.p, wires, 32 * pk->nb_wires, hipMemcpyHostToDevice, ctx->stream));
+  rc = pk->curve == GM_BN254 ? g16_prove_t<CurveBN254>(ctx, pk, w.p, da.p, db.p, dc.p, a, b, c, nc, r, s, ar_out,
+                                                       bs_out, krs_out)
+                             : g16_prove_t<CurveBLS12377>(ctx, pk, w.p, da.p, db.p, dc.p, a, b, c, nc, r, s, ar_out,
+                                                          bs_out, krs_out);
+  prof_collect(ctx);
+  return rc;
+}
+
+// ---- sharded Groth16 (one process per GPU) --------------------
+int gm_g16_partial_bytes(int curve, size_t* out) {
+  if (int rc = check_curve_id(curve)) return rc;
+  if (out) *out = 4 * 3 * fp_bytes(curve) + 3 * 2 * fp_bytes(curve);
+  return GM_OK;
+}
+
+int gm_g16_prove_partial(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, void* a_dev, void* b_dev, void* c_dev,
+                         size_t nc, void* partial_out) {
+  if (!ctx || !pk || !partial_out) return GM_ERR_INVALID;
+  if (nc > pk->n) {
+    set_error("prove: more constraints than the domain size");
+    return GM_ERR_INVALID;
+  }
+  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  GM_HIP(hipSetDevice(ctx->device));
+  auto run = [&](auto tag) -> int {
+    using C = decltype(tag);
+    DeviceH<C> hs(ctx, pk, a_dev, b_dev, c_dev, nc);
+    int rc;
+    if ((rc = hs.start())) return rc;
+    G16Sums<C> sums;
+    if ((rc = g16_sums_t<C>(ctx, pk, wires_dev, hs, sums, nullptr))) return rc;
+    sums_to_bytes<C>(sums, (uint8_t*)partial_out);
+    return GM_OK;
+  };
+  int rc = pk->curve == GM_BN254 ? run(CurveBN254()) : run(CurveBLS12377());
+  prof_collect(ctx);
+  return rc;
+}
+
+int gm_g16_finish(int curve, const gm_g16_pk_host* h, const void* sums, const void* r, const void* s, void* ar_out,
+                  void* bs_out, void* krs_out) {
+  if (int rc = check_curve_id(curve)) return rc;
+  if (!h || !sums || !r || !s || !ar_out || !bs_out || !krs_out) return GM_ERR_INVALID;
+  auto run = [&](auto tag) {
+    using C = decltype(tag);
+    G16Finish<C> fin((const uint8_t*)h->g1_alpha, (const uint8_t*)h->g1_beta, (const uint8_t*)h->g1_delta,
+                     (const uint8_t*)h->g2_beta, (const uint8_t*)h->g2_delta, r, s);
+    fin.begin();
+    G16Sums<C> sm;
+    bytes_to_sums<C>((const uint8_t*)sums, sm);
+    fin.finish(sm, ar_out, bs_out, krs_out);
+  };
+  if (curve == GM_BN254) run(CurveBN254());
+  else run(CurveBLS12377());
+  return GM_OK;
+}
+
+}  // extern "C"
+
+// ===========================================================================
+// single-process multi-device C-ABI (gm_multi)
+// ===========================================================================
+struct gm_multi {
+  std::vector<gm_ctx*> ctx;
+};
+
+struct gm_g16_pk_multi {
+  int curve;
+  std::vector<gm_g16_pk*> pk;  // pk[d] on ctx[d]
+};
+
+extern "C" {
+
+int gm_multi_init(const int* device_ids, int count, gm_multi** out) {
+  if (!device_ids || count < 1 || !out) return GM_ERR_INVALID;
+  auto* m = new gm_multi();
+  for (int d = 0; d < count; d++) {
+    gm_ctx* c = nullptr;
+    if (int rc = gm_init(device_ids[d], &c)) {
+      for (gm_ctx* x : m->ctx) gm_destroy(x);
+      delete m;
+      return rc;
+    }
+    m->ctx.push_back(c);
+  }
+  // direct xGMI copies device 0 -> d for the h slices (ignored when unsupported:
+  // HIP then stages peer copies itself)
+  for (int d = 1; d < count; d++) {
+    const int d0 = device_ids[0], dd = device_ids[d];
+    if (dd == d0) continue;
+    int can = 0;
+    if (hipDeviceCanAccessPeer(&can, dd, d0) == hipSuccess && can) {
+      hipSetDevice(dd);
+      hipDeviceEnablePeerAccess(d0, 0);
+      hipSetDevice(d0);
+      hipDeviceEnablePeerAccess(dd, 0);
+      (void)hipGetLastError();
+    }
+  }
+  *out = m;
+  return GM_OK;
+}
+
+int gm_multi_destroy(gm_multi* m) {
+  if (!m) return GM_OK;
+  for (gm_ctx* c : m->ctx) gm_destroy(c);
+  delete m;
+  return GM_OK;
+}
+
+int gm_multi_size(const gm_multi* m, int* count) {
+  if (!m || !count) return GM_ERR_INVALID;
+  *count = (int)m->ctx.size();
+  return GM_OK;
+}
+
+int gm_multi_context(gm_multi* m, int index, gm_ctx** out) {
+  if (!m || !out || index < 0 || index >= (int)m->ctx.size()) return GM_ERR_INVALID;
+  *out = m->ctx[index];
+  return GM_OK;
+}
+
+int gm_g16_pk_upload_multi(gm_multi* m, int curve, const gm_g16_pk_host* h, unsigned flags, gm_g16_pk_multi** out) {
+  if (!m || !h || !out || h->domain_size < 2) return GM_ERR_INVALID;
+  if (int rc = check_curve_id(curve)) return rc;
+  const int nd = (int)m->ctx.size();
+  // device 0 also runs computeH (~19 ms at 2^24): it takes a smaller share of
+  // the MSM work (GM_MULTI_SHARE0 = its weight relative to the others' 1.0)
+  std::vector<double> w(nd, 1.0);
+  if (nd > 1) {
+    const char* s0 = getenv("GM_MULTI_SHARE0");
+    w[0] = s0 ? std::max(0.0, atof(s0)) : 0.6;
+  }
+  auto* mp = new gm_g16_pk_multi();
+  mp->curve = curve;
+  mp->pk.assign(nd, nullptr);
+  std::vector<int> rcs(nd, GM_OK);
+  std::vector<std::string> errs(nd);
+  std::vector<std::thread> th;
+  for (int d = 0; d < nd; d++) {
+    th.emplace_back([&, d] {
+      gm_ctx* ctx = m->ctx[d];
+      std::lock_guard<std::recursive_mutex> g(ctx->mu);
+      if (hipSetDevice(ctx->device) != hipSuccess) {
+        rcs[d] = GM_ERR_DEVICE;
+        errs[d] = "hipSetDevice failed";
+        return;
+      }
+      Ranges rg;
+      shard_weighted(h->nbA, w, d, &rg.loA, &rg.hiA);
+      shard_weighted(h->nbB, w, d, &rg.loB, &rg.hiB);
+      shard_weighted(h->nbK, w, d, &rg.loK, &rg.hiK);
+      shard_weighted(h->domain_size - 1, w, d, &rg.loZ, &rg.hiZ);
+      rg.rebase = true;
+      gm_g16_pk_host hs = *h;
+      const size_t g1b = 2 * fp_bytes(curve), g2b = 4 * fp_bytes(curve);
+      hs.g1_A = (const uint8_t*)h->g1_A + g1b * rg.loA;
+      hs.g1_B = (const uint8_t*)h->g1_B + g1b * rg.loB;
+      hs.g1_K = (const uint8_t*)h->g1_K + g1b * rg.loK;
+      hs.g1_Z = (const uint8_t*)h->g1_Z + g1b * rg.loZ;
+      hs.g2_B = (const uint8_t*)h->g2_B + g2b * rg.loB;
+      rcs[d] = pk_upload_ranges(ctx, curve, &hs, flags, rg, &mp->pk[d]);
+      if (rcs[d]) errs[d] = gm_last_error();
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int d = 0; d < nd; d++)
+    if (rcs[d]) {
+      set_error("device " + std::to_string(d) + ": " + errs[d]);
+      for (int e = 0; e < nd; e++)
+        if (mp->pk[e]) gm_g16_pk_free(m->ctx[e], mp->pk[e]);
+      delete mp;
+      return rcs[d];
+    }
+  *out = mp;
+  return GM_OK;
+}
+
+int gm_g16_pk_free_multi(gm_multi* m, gm_g16_pk_multi* mp) {
+  if (!m || !mp) return GM_OK;
+  for (size_t d = 0; d < mp->pk.size() && d < m->ctx.size(); d++)
+    if (mp->pk[d]) gm_g16_pk_free(m->ctx[d], mp->pk[d]);
+  delete mp;
+  return GM_OK;
+}
+
+}  // extern "C"
+
+namespace gm {
+namespace {
+
+// All devices of `m` prove one proof: device d uploads only the wires its key
+// slices read ([wlo, whi)), runs its A/B/B2/K MSMs; device 0 additionally gets
+// a / b / c, runs computeH and copies each device's slice of h to it (xGMI peer
+// copies); every device then runs its Z slice.  The per-device sums are added
+// and finished on the host.
+template <class C>
+int g16_prove_multi_t(gm_multi* m, gm_g16_pk_multi* mp, const uint8_t* wires, const void* ha, const void* hb,
+                      const void* hc, size_t nc, const void* r, const void* s, void* ar_out, void* bs_out,
+                      void* krs_out) {
+  const int nd = (int)m->ctx.size();
+  gm_g16_pk* pk0 = mp->pk[0];
+  std::unique_ptr<G16Finish<C>> fin(make_finish<C>(pk0, r, s));
+  fin->begin();
+  SharedH sh;
+  std::vector<G16Sums<C>> sums(nd);
+  std::vector<int> rcs(nd, GM_OK);
+  std::vector<std::string> errs(nd);
+  // per-device h slice buffers, allocated up front so device 0 can address them
+  std::vector<std::unique_ptr<Arena>> arenas;
+  std::vector<void*> hz(nd, nullptr);
+  for (int d = 0; d < nd; d++) {
+    gm_ctx* ctx = m->ctx[d];
+    GM_HIP(hipSetDevice(ctx->device));
+    arenas.emplace_back(new Arena(ctx));
+    if (d > 0) {
+      DevBuf b;
+      if (int rc = b.alloc(*arenas[d], 32 * (mp->pk[d]->nbZ ? mp->pk[d]->nbZ : 1))) return rc;
+      hz[d] = b.p;
+    }
+  }
+  EventPair dist;
+  GM_HIP(hipSetDevice(m->ctx[0]->device));
+  if (int rc = dist.create()) return rc;
+  sh.done = dist.a;
+  auto worker = [&](int d) {
+    gm_ctx* ctx = m->ctx[d];
+    gm_g16_pk* pk = mp->pk[d];
+    auto fail = [&](int rc) {
+      rcs[d] = rc;
+      errs[d] = gm_last_error();
+      if (d == 0) {
+        std::lock_guard<std::mutex> lk(sh.mu);
+        if (!sh.ready) {
+          sh.ready = true;
+          sh.rc = rc;
+          sh.cv.notify_all();
+        }
+      }
+    };
+    std::lock_guard<std::recursive_mutex> g(ctx->mu);
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(GM_ERR_DEVICE);
+    Arena arena(ctx);
+    DevBuf w, da, db, dc;
+    const size_t nw = pk->whi - pk->wlo;
+    int rc;
+    if ((rc = w.alloc(arena, 32 * (nw ? nw : 1)))) return fail(rc);
+    if (nw && hipMemcpyAsync(w.p, wires + 32 * pk->wlo, 32 * nw, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+      return fail(GM_ERR_DEVICE);
+    std::unique_ptr<HSource> hs;
+    if (d == 0) {
+      if ((rc = da.alloc(arena, 32 * pk->n)) || (rc = db.alloc(arena, 32 * pk->n)) ||
+          (rc = dc.alloc(arena, 32 * pk->n)))
+        return fail(rc);
+      auto* x = new HostStagedH<C>(ctx, pk, da.p, db.p, dc.p, ha, hb, hc, nc);
+      hs.reset(x);
+      x->after_h = [&, x]() -> int {
+        // h is produced on ctx0->aux after x->ev.b: copy the slices there too
+        for (int e = 1; e < nd; e++) {
+          gm_g16_pk* pe = mp->pk[e];
+          if (!pe->nbZ) continue;
+          const void* src = (const char*)x->da + 32 * pe->zlo;
+          const int dev_e = m->ctx[e]->device;
+          if (dev_e == ctx->device)
+            GM_HIP(hipMemcpyAsync(hz[e], src, 32 * pe->nbZ, hipMemcpyDeviceToDevice, ctx->aux));
+          else
+            GM_HIP(hipMemcpyPeerAsync(hz[e], dev_e, src, ctx->device, 32 * pe->nbZ, ctx->aux));
+        }
+        GM_HIP(hipEventRecord(sh.done, ctx->aux));
+        std::lock_guard<std::mutex> lk(sh.mu);
+        sh.ready = true;
+        sh.cv.notify_all();
+        return GM_OK;
+      };
+      if ((rc = x->start())) return fail(rc);
+    } else {
+      hs.reset(new RemoteH(&sh, hz[d]));
+    }
+    if ((rc = g16_sums_t<C>(ctx, pk, w.p, *hs, sums[d], nullptr))) return fail(rc);
+    if (d == 0) {
+      // make sure h was produced (and distributed) even if device 0 has no Z slice
+      const void* zs;
+      if ((rc = hs->z_scalars(&zs))) return fail(rc);
+    }
+  };
+  std::vector<std::thread> th;
+  for (int d = 0; d < nd; d++) th.emplace_back(worker, d);
+  for (auto& t : th) t.join();
+  for (int d = 0; d < nd; d++) {
+    hipSetDevice(m->ctx[d]->device);
+    hipStreamSynchronize(m->ctx[d]->aux);
+    hipStreamSynchronize(m->ctx[d]->copy);
+  }
+  for (int d = 0; d < nd; d++)
+    if (rcs[d]) {
+      set_error("device " + std::to_string(d) + ": " + errs[d]);
+      return rcs[d];
+    }
+  G16Sums<C> tot = sums[0];
+  for (int d = 1; d < nd; d++) add_sums<C>(tot, sums[d]);
+  fin->finish(tot, ar_out, bs_out, krs_out);
+  // release the h slice buffers in LIFO order
+  while (!arenas.empty()) arenas.pop_back();
+  return GM_OK;
+}
+
+}  // namespace
+}  // namespace gm
+
+extern "C" {
+
+int gm_g16_prove_multi(gm_multi* m, gm_g16_pk_multi* mp, const void* wires, const void* a, const void* b,
+                       const void* c, size_t nc, const void* r, const void* s, void* ar_out, void* bs_out,
+                       void* krs_out) {
+  if (!m || !mp || !wires || !a || !b || !c || !r || !s || !ar_out || !bs_out || !krs_out) return GM_ERR_INVALID;
+  if (mp->pk.size() != m->ctx.size()) {
+    set_error("prove_multi: key uploaded to a different device set");
+    return GM_ERR_INVALID;
+  }
+  if (nc > mp->pk[0]->n) {
+    set_error("prove: more constraints than the domain size");
+    return GM_ERR_INVALID;
+  }
+  int rc = mp->curve == GM_BN254
+               ? g16_prove_multi_t<CurveBN254>(m, mp, (const uint8_t*)wires, a, b, c, nc, r, s, ar_out, bs_out, krs_out)
+               : g16_prove_multi_t<CurveBLS12377>(m, mp, (const uint8_t*)wires, a, b, c, nc, r, s, ar_out, bs_out,
+                                                  krs_out);
+  for (gm_ctx* x : m->ctx) prof_collect(x);
+  return rc;
+}
+
+}  // extern "C"

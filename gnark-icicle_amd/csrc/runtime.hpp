@@ -14,6 +14,7 @@
 namespace gm {
 
 void set_error(const std::string& msg);
+size_t fp_bytes(int curve);  // bytes of one base-field element (gnark layout)
 
 #define GM_HIP(call)                                                                      \
   do {                                                                                    \
@@ -35,7 +36,8 @@ struct KernelStat {
 struct gm_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  hipStream_t aux = nullptr;  // second stream: work overlapped with `stream` inside one call
+  hipStream_t aux = nullptr;   // second stream: work overlapped with `stream` inside one call
+  hipStream_t copy = nullptr;  // host->device input copies overlapped with kernels
   // pinned host staging for small device->host readbacks (truly async copies)
   void* pinned = nullptr;
   size_t pinned_cap = 0;

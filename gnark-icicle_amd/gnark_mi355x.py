@@ -47,7 +47,8 @@ SYMBOLS = [
     "gm_g16_pk_free", "gm_g16_prove", "gm_g16_prove_device", "gm_jac_add", "gm_jac_to_affine",
     "gm_batch_mul_base", "gm_random_scalars", "gm_generator", "gm_test_field_op",
     "gm_test_point_op", "gm_icicle_generate_twiddles", "gm_icicle_intt_on_device", "gm_icicle_ntt_on_device",
-    "gm_icicle_poly_ops",
+    "gm_icicle_poly_ops", "gm_device_count", "gm_multi_init", "gm_multi_destroy", "gm_multi_size",
+    "gm_multi_context", "gm_g16_pk_upload_multi", "gm_g16_pk_free_multi", "gm_g16_prove_multi",
 ]
 
 
@@ -116,6 +117,14 @@ def load_library(path: str = LIB_PATH):
     L.gm_icicle_intt_on_device.argtypes = [vp, i, vp, sz, i, pvp]
     L.gm_icicle_ntt_on_device.argtypes = [vp, i, vp, vp, sz, i]
     L.gm_icicle_poly_ops.argtypes = [vp, i, vp, vp, vp, vp, sz]
+    L.gm_device_count.argtypes = [ctypes.POINTER(i)]
+    L.gm_multi_init.argtypes = [ctypes.POINTER(i), i, pvp]
+    L.gm_multi_destroy.argtypes = [vp]
+    L.gm_multi_size.argtypes = [vp, ctypes.POINTER(i)]
+    L.gm_multi_context.argtypes = [vp, i, pvp]
+    L.gm_g16_pk_upload_multi.argtypes = [vp, i, vp, ctypes.c_uint, pvp]
+    L.gm_g16_pk_free_multi.argtypes = [vp, vp]
+    L.gm_g16_prove_multi.argtypes = [vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, vp, vp]
     _lib = L
     return L
 
@@ -591,6 +600,68 @@ class ProvingKey:
         _check(load_library().gm_g16_prove_partial(self.ctx.handle, self.handle, wires.ptr, a.ptr, b.ptr, c.ptr,
                                                    nb_constraints, _p(out)))
         return out.tobytes()
+
+
+class Multi:
+    """Several devices driven from ONE process (gm_multi): one context and host
+    thread per entry of device_ids (entries may repeat: several contexts on one
+    GPU rehearse the multi-GPU path).  The single-process seam gnark's
+    groth16.Prove needs (backend/groth16/groth16.go:192-204)."""
+
+    def __init__(self, device_ids):
+        ids = (ctypes.c_int * len(device_ids))(*device_ids)
+        h = ctypes.c_void_p()
+        _check(load_library().gm_multi_init(ids, len(device_ids), ctypes.byref(h)))
+        self.handle = h
+        self.device_ids = list(device_ids)
+
+    def close(self):
+        if self.handle:
+            load_library().gm_multi_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+class ProvingKeyMulti:
+    """A proving key sharded across the devices of a Multi (gm_g16_pk_upload_multi)."""
+
+    def __init__(self, multi: Multi, curve, pk: dict, domain_size: int, nb_wires: int, nb_public: int,
+                 precompute: bool = False):
+        self.multi = multi
+        self.curve = curve_id(curve)
+        h, arrs = _pk_host_struct(curve, pk, domain_size, nb_wires, nb_public)
+        self._keep, self._h = arrs, h
+        handle = ctypes.c_void_p()
+        _check(load_library().gm_g16_pk_upload_multi(multi.handle, self.curve, ctypes.byref(h),
+                                                     ProvingKey.PRECOMPUTE if precompute else 0,
+                                                     ctypes.byref(handle)))
+        self.handle = handle
+
+    def free(self):
+        if self.handle:
+            load_library().gm_g16_pk_free_multi(self.multi.handle, self.handle)
+            self.handle = None
+
+    def prove(self, wires, a, b, c, r: bytes, s: bytes):
+        """(Ar, Bs, Krs) affine bytes; wires / a / b / c in host memory."""
+        W, A, B, C, R, S = (_buf(x) for x in (wires, a, b, c, r, s))
+        ar = np.zeros(point_bytes(self.curve, False), np.uint8)
+        krs = np.zeros(point_bytes(self.curve, False), np.uint8)
+        bs = np.zeros(point_bytes(self.curve, True), np.uint8)
+        _check(load_library().gm_g16_prove_multi(self.multi.handle, self.handle, _p(W), _p(A), _p(B), _p(C),
+                                                 A.size // FR_BYTES, _p(R), _p(S), _p(ar), _p(bs), _p(krs)))
+        return ar.tobytes(), bs.tobytes(), krs.tobytes()
+
+
+def device_count() -> int:
+    n = ctypes.c_int()
+    _check(load_library().gm_device_count(ctypes.byref(n)))
+    return n.value
 
 
 def g16_partial_bytes(curve) -> int:

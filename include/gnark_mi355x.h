@@ -44,7 +44,9 @@ typedef struct gm_ctx gm_ctx;
 /* ---- context ---------------------------------------------------------- */
 const char* gm_last_error(void);
 int gm_version(void);
-/* Creates a context on HIP device `device` with its own stream. */
+/* Number of visible HIP devices. */
+int gm_device_count(int* count);
+/* Creates a context on HIP device `device` with its own streams. */
 int gm_init(int device, gm_ctx** out);
 int gm_destroy(gm_ctx* ctx);
 int gm_synchronize(gm_ctx* ctx);
@@ -208,7 +210,9 @@ int gm_g16_pk_free(gm_ctx* ctx, gm_g16_pk* pk);
 
 /* Proves with solved vectors in host memory: wires (nb_wires Fr), a, b, c
  * (nb_constraints Fr each), r and s (one Fr each, Montgomery).  Outputs
- * proof.Ar (G1Affine), proof.Bs (G2Affine), proof.Krs (G1Affine). */
+ * proof.Ar (G1Affine), proof.Bs (G2Affine), proof.Krs (G1Affine).  The wires
+ * are copied first; a, b, c are copied on a separate stream by a helper thread
+ * while the A/B/K MSMs run (the icicle.go:204-412 scope, H2D included). */
 int gm_g16_prove(gm_ctx* ctx, gm_g16_pk* pk, const void* wires, const void* a, const void* b,
                  const void* c, size_t nb_constraints, const void* r, const void* s,
                  void* ar_out, void* bs_out, void* krs_out);
@@ -241,6 +245,33 @@ int gm_g16_prove_partial(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, void
  * [-rs]delta, [s]Ar, [r]Bs1, [s]delta2, beta2 from `pk`). */
 int gm_g16_finish(int curve, const gm_g16_pk_host* pk, const void* sums, const void* r, const void* s,
                   void* ar_out, void* bs_out, void* krs_out);
+
+/* ---- single-process multi-device Groth16 (one gnark process drives every
+ *      GPU of the node behind unchanged groth16.Prove call sites,
+ *      backend/groth16/groth16.go:192-204) ---------------
+ * gm_multi_init creates one context (own streams) per entry of device_ids
+ * (entries may repeat: several contexts on one GPU rehearse the multi-GPU path).
+ * gm_g16_pk_upload_multi shards every point array of the key across the
+ * devices (device 0, which also runs computeH, takes a smaller share:
+ * GM_MULTI_SHARE0, default 0.6 of the others'); each device keeps only the
+ * compaction-map slices of its shard and later receives only the wires those
+ * slices read.  gm_g16_prove_multi runs one host thread per device: wires
+ * slices to every device, a / b / c to device 0 (computeH there, h slices sent
+ * to the other devices by peer copies over xGMI), the five partial MSMs
+ * everywhere, then host adds of the per-device sums and the finishing of
+ * gm_g16_finish.  Output and inputs as gm_g16_prove. */
+typedef struct gm_multi gm_multi;
+typedef struct gm_g16_pk_multi gm_g16_pk_multi;
+int gm_multi_init(const int* device_ids, int count, gm_multi** out);
+int gm_multi_destroy(gm_multi* m);
+int gm_multi_size(const gm_multi* m, int* count);
+int gm_multi_context(gm_multi* m, int index, gm_ctx** out);
+int gm_g16_pk_upload_multi(gm_multi* m, int curve, const gm_g16_pk_host* pk, unsigned flags,
+                           gm_g16_pk_multi** out);
+int gm_g16_pk_free_multi(gm_multi* m, gm_g16_pk_multi* pk);
+int gm_g16_prove_multi(gm_multi* m, gm_g16_pk_multi* pk, const void* wires, const void* a, const void* b,
+                       const void* c, size_t nb_constraints, const void* r, const void* s, void* ar_out,
+                       void* bs_out, void* krs_out);
 
 /* ---- host-side group helpers (finishing adds of sharded MSMs) ---------- */
 /* out = p + q, all gnark Jacobian (G1Jac or G2Jac). */

@@ -1,0 +1,252 @@
+// Package gm is the cgo binding of libgnark_mi355x (include/gnark_mi355x.h)
+// shared by the gnark hooks in this directory (icicle_bn254, icicle_bls12377,
+// plonk_bls12377) and by the iciclegnark-compatible shim
+// (iciclegnark/curves/bn254).
+//
+// NOT COMPILED HERE: this image has no Go toolchain.  The C side it binds is
+// built and tested by the repo (tests/test_capi_symbols.py, tests/*_gpu.py).
+//
+// Devices: GNARK_MI355X_DEVICES="0,1,..." selects the GPUs one process drives
+// (default: every visible device).  With more than one, Groth16 keys are
+// sharded across them (gm_g16_pk_upload_multi) and proofs run on all of them
+// from the one gnark process (gm_g16_prove_multi) -- groth16.Prove's call
+// sites (backend/groth16/groth16.go:192-204) stay unchanged.
+package gm
+
+/*
+#cgo CFLAGS: -I${SRCDIR}/../../../include
+#cgo LDFLAGS: -L${SRCDIR}/../../../gnark-icicle_amd -lgnark_mi355x -Wl,-rpath,${SRCDIR}/../../../gnark-icicle_amd
+#include <stdlib.h>
+#include "gnark_mi355x.h"
+*/
+import "C"
+
+import (
+	"errors"
+	"fmt"
+	"os"
+	"strconv"
+	"strings"
+	"sync"
+	"unsafe"
+)
+
+// Curve ids of the C-ABI.
+const (
+	BN254     = C.GM_BN254
+	BLS12_377 = C.GM_BLS12_377
+)
+
+// PkPrecompute keeps fixed-base window copies of every proving-key point array
+// on the device(s) (GM_PK_PRECOMPUTE).
+const PkPrecompute = C.GM_PK_PRECOMPUTE
+
+func lastErr(what string, rc C.int) error {
+	return fmt.Errorf("gnark_mi355x %s: status %d: %s", what, int(rc), C.GoString(C.gm_last_error()))
+}
+
+var (
+	once    sync.Once
+	devices []C.int
+	ctx0    *C.gm_ctx  // context on devices[0]: MSM / NTT / KZG calls
+	multi   *C.gm_multi // all devices (nil when only one)
+	initErr error
+)
+
+func initDevices() {
+	var n C.int
+	if rc := C.gm_device_count(&n); rc != C.GM_OK {
+		initErr = lastErr("gm_device_count", rc)
+		return
+	}
+	if s := os.Getenv("GNARK_MI355X_DEVICES"); s != "" {
+		for _, f := range strings.Split(s, ",") {
+			d, err := strconv.Atoi(strings.TrimSpace(f))
+			if err != nil {
+				initErr = fmt.Errorf("GNARK_MI355X_DEVICES: %w", err)
+				return
+			}
+			devices = append(devices, C.int(d))
+		}
+	} else {
+		for d := C.int(0); d < n; d++ {
+			devices = append(devices, d)
+		}
+	}
+	if len(devices) == 0 {
+		initErr = errors.New("gnark_mi355x: no GPU visible")
+		return
+	}
+	if rc := C.gm_init(devices[0], &ctx0); rc != C.GM_OK {
+		initErr = lastErr("gm_init", rc)
+		return
+	}
+	if len(devices) > 1 {
+		if rc := C.gm_multi_init(&devices[0], C.int(len(devices)), &multi); rc != C.GM_OK {
+			initErr = lastErr("gm_multi_init", rc)
+		}
+	}
+}
+
+// Ctx returns the context of the first selected device.
+func Ctx() (*C.gm_ctx, error) {
+	once.Do(initDevices)
+	return ctx0, initErr
+}
+
+// NbDevices is the number of GPUs this process proves on.
+func NbDevices() int {
+	once.Do(initDevices)
+	return len(devices)
+}
+
+// ---------------------------------------------------------------------------
+// Groth16
+// ---------------------------------------------------------------------------
+
+// G16HostKey mirrors gm_g16_pk_host: the gnark proving-key arrays, passed by
+// pointer (gnark-crypto's G1Affine / G2Affine / fr.Element layouts are the
+// C-ABI's), read only during the upload.
+type G16HostKey struct {
+	DomainSize, NbWires, NbPublic uint64
+	NbA, NbB, NbK                 uint64
+	Alpha, Beta, Delta            unsafe.Pointer // *G1Affine
+	A, B, Z, K                    unsafe.Pointer // first element of each []G1Affine
+	Beta2, Delta2                 unsafe.Pointer // *G2Affine
+	B2                            unsafe.Pointer // first element of []G2Affine
+	InfA, InfB                    []bool         // pk.InfinityA / InfinityB
+	KWires                        []uint32       // nil, or the filterHeap survivors (prove.go:243-245)
+}
+
+// G16Key is a proving key resident on the GPU(s) (setupDevicePointers,
+// icicle.go:31-130).
+type G16Key struct {
+	curve  C.int
+	single *C.gm_g16_pk
+	multi  *C.gm_g16_pk_multi
+}
+
+func boolsToBytes(b []bool) []byte {
+	out := make([]byte, len(b))
+	for i, v := range b {
+		if v {
+			out[i] = 1
+		}
+	}
+	return out
+}
+
+// UploadG16Key uploads k once (sharded across the GPUs when there are several).
+func UploadG16Key(curve int, k *G16HostKey, flags uint) (*G16Key, error) {
+	ctx, err := Ctx()
+	if err != nil {
+		return nil, err
+	}
+	infA, infB := boolsToBytes(k.InfA), boolsToBytes(k.InfB)
+	h := C.gm_g16_pk_host{
+		domain_size: C.size_t(k.DomainSize), nb_wires: C.size_t(k.NbWires), nb_public: C.size_t(k.NbPublic),
+		nbA: C.size_t(k.NbA), nbB: C.size_t(k.NbB), nbK: C.size_t(k.NbK),
+		g1_alpha: k.Alpha, g1_beta: k.Beta, g1_delta: k.Delta,
+		g1_A: k.A, g1_B: k.B, g1_Z: k.Z, g1_K: k.K,
+		g2_beta: k.Beta2, g2_delta: k.Delta2, g2_B: k.B2,
+		infA: (*C.uint8_t)(unsafe.Pointer(&infA[0])), infB: (*C.uint8_t)(unsafe.Pointer(&infB[0])),
+	}
+	if len(k.KWires) > 0 {
+		h.k_wires = (*C.uint32_t)(unsafe.Pointer(&k.KWires[0]))
+	}
+	key := &G16Key{curve: C.int(curve)}
+	if multi != nil {
+		if rc := C.gm_g16_pk_upload_multi(multi, C.int(curve), &h, C.uint(flags), &key.multi); rc != C.GM_OK {
+			return nil, lastErr("gm_g16_pk_upload_multi", rc)
+		}
+	} else if rc := C.gm_g16_pk_upload_ex(ctx, C.int(curve), &h, C.uint(flags), &key.single); rc != C.GM_OK {
+		return nil, lastErr("gm_g16_pk_upload_ex", rc)
+	}
+	return key, nil
+}
+
+// Free releases the device copies.
+func (k *G16Key) Free() {
+	if k.multi != nil {
+		C.gm_g16_pk_free_multi(multi, k.multi)
+	}
+	if k.single != nil {
+		C.gm_g16_pk_free(ctx0, k.single)
+	}
+}
+
+// Prove runs the device part of the Groth16 prover (icicle.go:204-412 /
+// prove.go:140-313): computeH, the compaction, the five MSMs and the finishing
+// adds.  wires, a, b, c point at the first fr.Element of solution.W, .A, .B,
+// .C; r, s at the sampled fr.Elements; ar, krs at G1Affine and bs at G2Affine.
+func (k *G16Key) Prove(wires, a, b, c unsafe.Pointer, nbConstraints int, r, s, ar, bs, krs unsafe.Pointer) error {
+	if k.multi != nil {
+		if rc := C.gm_g16_prove_multi(multi, k.multi, wires, a, b, c, C.size_t(nbConstraints), r, s, ar, bs, krs); rc != C.GM_OK {
+			return lastErr("gm_g16_prove_multi", rc)
+		}
+		return nil
+	}
+	if rc := C.gm_g16_prove(ctx0, k.single, wires, a, b, c, C.size_t(nbConstraints), r, s, ar, bs, krs); rc != C.GM_OK {
+		return lastErr("gm_g16_prove", rc)
+	}
+	return nil
+}
+
+// ---------------------------------------------------------------------------
+// KZG (PLONK)
+// ---------------------------------------------------------------------------
+
+// SRS is a KZG SRS (pk.Kzg.G1 or pk.KzgLagrange.G1) resident on device 0.
+type SRS struct {
+	curve C.int
+	dev   unsafe.Pointer
+	n     int
+}
+
+// UploadSRS keeps the n G1Affine points at pts on the GPU.
+func UploadSRS(curve int, pts unsafe.Pointer, n int) (*SRS, error) {
+	ctx, err := Ctx()
+	if err != nil {
+		return nil, err
+	}
+	s := &SRS{curve: C.int(curve), n: n}
+	if rc := C.gm_points_upload(ctx, C.int(curve), 0, pts, C.size_t(n), &s.dev); rc != C.GM_OK {
+		return nil, lastErr("gm_points_upload", rc)
+	}
+	return s, nil
+}
+
+// Commit writes sum_i coeffs[i] * srs[i] (kzg.Commit) as a G1Affine at digest.
+func (s *SRS) Commit(coeffs unsafe.Pointer, n int, digest unsafe.Pointer) error {
+	if rc := C.gm_kzg_commit(ctx0, s.curve, s.dev, C.size_t(s.n), coeffs, C.size_t(n), digest); rc != C.GM_OK {
+		return lastErr("gm_kzg_commit", rc)
+	}
+	return nil
+}
+
+// NTT runs an in-place fft.Domain FFT / FFTInverse of n fr.Elements at data
+// (host memory; copied to and from device 0).
+func NTT(curve int, data unsafe.Pointer, n int, inverse, dit, coset bool) error {
+	ctx, err := Ctx()
+	if err != nil {
+		return err
+	}
+	b := func(v bool) C.int {
+		if v {
+			return 1
+		}
+		return 0
+	}
+	var dev unsafe.Pointer
+	if rc := C.gm_copy_to_device(ctx, data, C.size_t(32*n), &dev); rc != C.GM_OK {
+		return lastErr("gm_copy_to_device", rc)
+	}
+	defer C.gm_free(ctx, dev)
+	if rc := C.gm_ntt(ctx, C.int(curve), dev, C.size_t(n), b(inverse), b(dit), b(coset)); rc != C.GM_OK {
+		return lastErr("gm_ntt", rc)
+	}
+	if rc := C.gm_memcpy_d2h(ctx, data, dev, C.size_t(32*n)); rc != C.GM_OK {
+		return lastErr("gm_memcpy_d2h", rc)
+	}
+	return nil
+}

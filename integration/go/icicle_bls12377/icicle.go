@@ -1,0 +1,224 @@
+//go:build icicle
+
+// Package icicle_bls12377 -- MI355X GPU hook for BLS12-377 Groth16 (BASELINE configs[4]); the
+// reference has no GPU path for this curve (SURVEY.md §0.2).  Same template as
+// icicle_bn254: backend/groth16/bls12-377/prove.go:62-325 is the BN254 prover
+// modulo curve names, so only the package names and the gm curve id differ.
+//
+// Re-derived from the CURRENT CPU prover groth16_bls12377.Prove
+// (backend/groth16/bls12-377/prove.go:62-325), not from the stale icicle.go
+// (SURVEY.md §0.3: icicle.go:160 reads a HintID field constraint.Groth16Commitment
+// no longer has, :44,47 read fft.Domain internals).  Everything before the
+// device block is prove.go's own flow -- the BSB22 commitment hint, Solve, the
+// proof-of-knowledge fold (prove.go:82-139) -- and the whole device block
+// (computeH, compaction, 4 G1 + 1 G2 MSMs, finishing adds; prove.go:140-313,
+// icicle.go:204-412) is ONE call into libgnark_mi355x: gm_g16_prove (one GPU) or
+// gm_g16_prove_multi (the key sharded over every GPU of the node).
+//
+// NOT COMPILED HERE: this image has no Go toolchain.  The device block is the
+// tested C-ABI (tests/test_groth16_gpu.py, tests/test_configs_full.py).
+package icicle_bls12377
+
+import (
+	"fmt"
+	"math/big"
+	"unsafe"
+
+	"github.com/consensys/gnark-crypto/ecc"
+	curve "github.com/consensys/gnark-crypto/ecc/bls12-377"
+	"github.com/consensys/gnark-crypto/ecc/bls12-377/fr"
+	"github.com/consensys/gnark-crypto/ecc/bls12-377/fr/hash_to_field"
+	"github.com/consensys/gnark/backend"
+	groth16_bls12377 "github.com/consensys/gnark/backend/groth16/bls12-377"
+	"github.com/consensys/gnark/backend/witness"
+	"github.com/consensys/gnark/constraint"
+	cs "github.com/consensys/gnark/constraint/bls12-377"
+	"github.com/consensys/gnark/constraint/solver"
+	fcs "github.com/consensys/gnark/frontend/cs"
+	"github.com/consensys/gnark/logger"
+
+	"github.com/consensys/gnark/backend/accel/mi355x/gm"
+)
+
+const HasIcicle = true
+
+// kWires lists, for every point of pk.G1.K, the wire whose value multiplies it:
+// the private wires minus the private-committed and commitment wires, i.e. the
+// survivors of prove.go:243-245's filterHeap, as absolute wire indices.
+func kWires(r1cs *cs.R1CS, nbWires int) []uint32 {
+	info := r1cs.CommitmentInfo.(constraint.Groth16Commitments)
+	drop := map[int]bool{}
+	for _, i := range info.GetPrivateCommitted() {
+		drop[i] = true
+	}
+	for _, i := range info.CommitmentIndexes() {
+		drop[i] = true
+	}
+	if len(drop) == 0 {
+		return nil // gm default: K[i] <-> wire nbPublic + i
+	}
+	out := make([]uint32, 0, nbWires)
+	for i := r1cs.GetNbPublicVariables(); i < nbWires; i++ {
+		if !drop[i] {
+			out = append(out, uint32(i))
+		}
+	}
+	return out
+}
+
+// setupDevicePointers uploads the key once (icicle.go:31-130).  The point arrays
+// are converted to the MSM layout on the device; GNARK_MI355X_PRECOMPUTE=1 also
+// keeps fixed-base window copies (~12x the point memory, -20% prove time at 2^24).
+func (pk *ProvingKey) setupDevicePointers(r1cs *cs.R1CS) error {
+	if pk.deviceInfo != nil {
+		return nil
+	}
+	nbWires := len(pk.InfinityA)
+	k := &gm.G16HostKey{
+		DomainSize: pk.Domain.Cardinality, NbWires: uint64(nbWires),
+		NbPublic: uint64(r1cs.GetNbPublicVariables()),
+		NbA:      uint64(len(pk.G1.A)), NbB: uint64(len(pk.G1.B)), NbK: uint64(len(pk.G1.K)),
+		Alpha:    unsafe.Pointer(&pk.G1.Alpha), Beta: unsafe.Pointer(&pk.G1.Beta), Delta: unsafe.Pointer(&pk.G1.Delta),
+		Beta2:    unsafe.Pointer(&pk.G2.Beta), Delta2: unsafe.Pointer(&pk.G2.Delta),
+		InfA:     pk.InfinityA, InfB: pk.InfinityB,
+		KWires:   kWires(r1cs, nbWires),
+	}
+	first := func(n int, p unsafe.Pointer) unsafe.Pointer {
+		if n == 0 {
+			return nil
+		}
+		return p
+	}
+	k.A = first(len(pk.G1.A), unsafe.Pointer(&pk.G1.A[0]))
+	k.B = first(len(pk.G1.B), unsafe.Pointer(&pk.G1.B[0]))
+	k.Z = first(len(pk.G1.Z), unsafe.Pointer(&pk.G1.Z[0]))
+	k.K = first(len(pk.G1.K), unsafe.Pointer(&pk.G1.K[0]))
+	k.B2 = first(len(pk.G2.B), unsafe.Pointer(&pk.G2.B[0]))
+	flags := uint(0)
+	if precomputeRequested() {
+		flags |= gm.PkPrecompute
+	}
+	key, err := gm.UploadG16Key(gm.BLS12_377, k, flags)
+	if err != nil {
+		return err
+	}
+	pk.deviceInfo = &deviceInfo{key: key}
+	return nil
+}
+
+// bsb22Hint is the BSB22 commitment hint of prove.go:82-109: it commits to the
+// private committed values with the Pedersen key, hashes the commitment with
+// the public/commitment-committed inputs to the field and returns that as the
+// commitment wire's value.
+func bsb22Hint(pk *ProvingKey, info constraint.Groth16Commitments, proof *groth16_bls12377.Proof,
+	committed [][]fr.Element, opt *backend.ProverConfig) solver.Hint {
+	return func(_ *big.Int, in []*big.Int, out []*big.Int) error {
+		i := int(in[0].Int64())
+		args := in[1:]
+		nbHashed := len(info[i].PublicAndCommitmentCommitted)
+		hashed, priv := args[:nbHashed], args[nbHashed:]
+		committed[i] = make([]fr.Element, len(info[i].PrivateCommitted))
+		for j := range priv {
+			committed[i][j].SetBigInt(priv[j])
+		}
+		var err error
+		if proof.Commitments[i], err = pk.CommitmentKeys[i].Commit(committed[i]); err != nil {
+			return err
+		}
+		h := opt.HashToFieldFn
+		h.Write(constraint.SerializeCommitment(proof.Commitments[i].Marshal(), hashed, (fr.Bits-1)/8+1))
+		digest := h.Sum(nil)
+		h.Reset()
+		take := fr.Bytes
+		if h.Size() < take {
+			take = h.Size()
+		}
+		var v fr.Element
+		v.SetBytes(digest[:take])
+		v.BigInt(out[0])
+		return nil
+	}
+}
+
+// foldPok computes proof.CommitmentPok (prove.go:113-139): one proof of
+// knowledge per commitment key, folded with a challenge hashed from the
+// commitment wires' values.
+func foldPok(pk *ProvingKey, info constraint.Groth16Commitments, w []fr.Element, committed [][]fr.Element,
+	proof *groth16_bls12377.Proof) error {
+	poks := make([]curve.G1Affine, len(pk.CommitmentKeys))
+	for i := range pk.CommitmentKeys {
+		var err error
+		if poks[i], err = pk.CommitmentKeys[i].ProveKnowledge(committed[i]); err != nil {
+			return err
+		}
+	}
+	ser := make([]byte, fr.Bytes*len(info))
+	for i := range info {
+		copy(ser[fr.Bytes*i:], w[info[i].CommitmentIndex].Marshal())
+	}
+	challenge, err := fr.Hash(ser, []byte("G16-BSB22"), 1)
+	if err != nil {
+		return err
+	}
+	_, err = proof.CommitmentPok.Fold(poks, challenge[0], ecc.MultiExpConfig{NbTasks: 1})
+	return err
+}
+
+// Prove generates the proof of knowledge of a r1cs with full witness (secret +
+// public part) on the MI355X GPU(s).  Same signature, options, errors and proof
+// bytes as groth16_bls12377.Prove (given the same crypto/rand stream for r, s).
+func Prove(r1cs *cs.R1CS, pk *ProvingKey, fullWitness witness.Witness, opts ...backend.ProverOption) (*groth16_bls12377.Proof, error) {
+	opt, err := backend.NewProverConfig(opts...)
+	if err != nil {
+		return nil, fmt.Errorf("new prover config: %w", err)
+	}
+	if opt.HashToFieldFn == nil {
+		opt.HashToFieldFn = hash_to_field.New([]byte(constraint.CommitmentDst))
+	}
+	if opt.Accelerator != "icicle" {
+		return groth16_bls12377.Prove(r1cs, &pk.ProvingKey, fullWitness, opts...)
+	}
+	log := logger.Logger().With().Str("curve", r1cs.CurveID().String()).Str("acceleration", "mi355x").
+		Int("nbConstraints", r1cs.GetNbConstraints()).Int("gpus", gm.NbDevices()).Str("backend", "groth16").Logger()
+	if err := pk.setupDevicePointers(r1cs); err != nil {
+		return nil, fmt.Errorf("setup device pointers: %w", err)
+	}
+
+	info := r1cs.CommitmentInfo.(constraint.Groth16Commitments)
+	proof := &groth16_bls12377.Proof{Commitments: make([]curve.G1Affine, len(info))}
+	committed := make([][]fr.Element, len(info))
+	solverOpts := append(opt.SolverOpts[:len(opt.SolverOpts):len(opt.SolverOpts)],
+		solver.OverrideHint(solver.GetHintID(fcs.Bsb22CommitmentComputePlaceholder),
+			bsb22Hint(pk, info, proof, committed, &opt)))
+
+	sol, err := r1cs.Solve(fullWitness, solverOpts...)
+	if err != nil {
+		return nil, err
+	}
+	solution := sol.(*cs.R1CSSolution)
+	w := []fr.Element(solution.W)
+
+	if err := foldPok(pk, info, w, committed, proof); err != nil {
+		return nil, err
+	}
+
+	// r, s sampled exactly as prove.go:183-188 (same crypto/rand stream ->
+	// byte-identical proofs on the CPU and the GPU path)
+	var r, s fr.Element
+	if _, err := r.SetRandom(); err != nil {
+		return nil, err
+	}
+	if _, err := s.SetRandom(); err != nil {
+		return nil, err
+	}
+
+	nbCons := len(solution.A)
+	if err := pk.deviceInfo.key.Prove(unsafe.Pointer(&w[0]), unsafe.Pointer(&solution.A[0]),
+		unsafe.Pointer(&solution.B[0]), unsafe.Pointer(&solution.C[0]), nbCons,
+		unsafe.Pointer(&r), unsafe.Pointer(&s),
+		unsafe.Pointer(&proof.Ar), unsafe.Pointer(&proof.Bs), unsafe.Pointer(&proof.Krs)); err != nil {
+		return nil, err
+	}
+	log.Debug().Msg("prover done")
+	return proof, nil
+}

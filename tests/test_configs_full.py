@@ -132,6 +132,24 @@ def test_groth16_2p20_sharded_world8(gm_ctx, chain_2p20):
     assert got == d["exp"]
 
 
+@pytest.mark.parametrize("ndev,precompute", [(4, False), (3, True)])
+def test_groth16_2p20_multi_contexts(chain_2p20, ndev, precompute):
+    """Single-process multi-device prove (gm_g16_prove_multi) with `ndev`
+    contexts on the one test GPU: sharded key (device 0 lighter), wire slices,
+    computeH on device 0, h slices copied to the others, host-summed partials."""
+    import gnark_mi355x as gm
+    d = chain_2p20
+    r1 = d["r1"]
+    with gm.Multi([0] * ndev) as m:
+        mpk = gm.ProvingKeyMulti(m, d["cname"], d["pk"], r1.domain_size, r1.nb_wires, r1.nb_public,
+                                 precompute=precompute)
+        try:
+            got = mpk.prove(d["W"], d["a"], d["b"], d["c"], d["r"], d["s"])
+        finally:
+            mpk.free()
+    assert got == d["exp"]
+
+
 @pytest.mark.parametrize("g2", [False, True])
 def test_msm_bls12377_2p22_vs_oracle(gm_ctx, oracle, g2):
     """configs[4]: BLS12-377 G1 / G2 MSM at 2^22, uniform scalars, random points."""

@@ -151,3 +151,27 @@ def test_groth16_sharded_partials(gm_ctx, oracle, cname, k, world, precompute):
             dpk.free()
     got = gm.g16_finish(cname, dpk._h, gm.g16_reduce_partials(cname, parts), rb, sb)
     assert got == exp
+
+
+@pytest.mark.parametrize("cname,k,ndev", [("bn254", 1023, 2), ("bn254", 15, 5), ("bls12377", 511, 3)])
+def test_groth16_multi_contexts_small(gm_ctx, oracle, cname, k, ndev):
+    """gm_g16_prove_multi on `ndev` contexts of the one GPU (ragged and tiny
+    shards at n = 16 with 5 devices): byte-identical to the CPU restatement and
+    accepted by the exponent check."""
+    import gnark_mi355x as gm
+    c = pyref.CURVES[cname]
+    r1, W = R.squaring_chain(k, cname, x=9)
+    tox = R.encode_vec(cname, [t % c.r for t in TOXIC])
+    pk = oracle.g16_setup(cname, r1, tox)
+    a, b, cc = r1.solve_abc(W)
+    enc = lambda v: R.encode_vec(cname, v)
+    rb, sb = enc([0x1111]), enc([0x2222])
+    exp = oracle.g16_prove(cname, pk, r1.nb_public, enc(W), enc(a), enc(b), enc(cc), rb, sb)
+    with gm.Multi([0] * ndev) as m:
+        mpk = gm.ProvingKeyMulti(m, cname, pk, r1.domain_size, r1.nb_wires, r1.nb_public)
+        try:
+            got = mpk.prove(enc(W), enc(a), enc(b), enc(cc), rb, sb)
+        finally:
+            mpk.free()
+    assert got == exp
+    assert oracle.g16_check(cname, r1, tox, enc(W), rb, sb, *got) == 7
