@@ -8,9 +8,21 @@ struct gm_ctx;
 
 namespace gm {
 struct Arena;
-// Sorts M (key, value) u32 pairs by the low end_bit key bits (msm_sort.hip).
-int msm_sort_pairs(gm_ctx* ctx, Arena& arena, const uint32_t* keys_in, uint32_t* keys_out,
-                   const uint32_t* vals_in, uint32_t* vals_out, size_t M, int end_bit);
+// Two-level counting sort of the MSM digits (msm_impl.hpp pass 1, msm_sort.hip
+// pass 2).  T buckets; coarse bin H = bucket >> F (NC bins); M = upper bound on
+// the entries.  Coarse bins above S2_BIG entries are split into parts.
+constexpr uint32_t S2_BIG = 1u << 16;
+constexpr uint32_t S2_STAGE = 6144;  // bins up to this many entries are sorted in LDS
+struct SortGeom {
+  uint32_t T = 0, F = 0, NC = 0;
+  size_t M = 0;
+};
+// Digits (k_msm_digits output, window-major, with the coarse counts) ->
+// sorted keys / values and offsets[0..T].  Scratch: cbase / pbase (NC + 1),
+// ccursor (NC), tmp (8 B x M), fcount (T).
+int msm_sort_digits(gm_ctx* ctx, const SortGeom& g, size_t n, uint32_t W, uint32_t nb, uint32_t shared_stride,
+                    const uint32_t* dig, const uint32_t* ccount, uint32_t* cbase, uint32_t* ccursor, uint32_t* pbase,
+                    uint64_t* tmp, uint32_t* fcount, uint32_t* keys_out, uint32_t* vals_out, uint32_t* offsets);
 
 // Fixed-base precomputation of a resident point set (a proving key's arrays):
 // W copies of the n points, copy w = [2^(c w)] P_i at index w * stride + i, so
@@ -33,11 +45,10 @@ MsmPrecomp msm_choose_precomp(size_t n, int bits);
 struct MsmPlan {
   uint32_t c = 0, W = 0, nb = 0, total = 0;
   uint32_t Wred = 0;  // windows reduced separately: W (plain) or 1 (shared buckets)
-  uint32_t dW = 0;    // digit-major keys with dW windows (KeyFmt, msm_impl.hpp), 0 = window-major
-  size_t n = 0, M = 0;
+  size_t n = 0, M = 0;  // M: upper bound on the sorted entries (n * W); offsets[total] = actual
   size_t npts = 0;    // points addressable through the plan (bounds check)
-  uint32_t* keys = nullptr;     // sorted bucket keys, M entries
-  uint32_t* vals = nullptr;     // point index | sign << 31, M entries
+  uint32_t* keys = nullptr;     // sorted bucket keys (window-major bucket index), offsets[total] entries
+  uint32_t* vals = nullptr;     // point index | sign << 31
   uint32_t* offsets = nullptr;  // total + 1 bucket start offsets
 };
 template <class C>

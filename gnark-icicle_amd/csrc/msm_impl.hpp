@@ -3,23 +3,24 @@
 // MsmG2OnDevice (backend/groth16/bn254/icicle/icicle.go:302,315,332,355,382).
 //
 // Pipeline (one HIP stream, all state in HBM; msm_plan + msm_run below):
-//   1. k_msm_keys       Montgomery -> canonical scalar, signed c-bit digits of all
-//                       W windows -> (bucket key, point index | sign << 31) pairs;
-//                       digit-major keys (KeyFmt) when that saves a radix pass.
-//   2. radix sort of the pairs by key (msm_sort_pairs, msm_sort.hip).
-//   3. k_msm_bounds (+ k_msm_bounds_fill) or k_msm_lower_bound: bucket start
-//      offsets in the sorted list.
-//   4. k_msm_accum_seg  load-balanced slices of K sorted entries per thread:
+//   1. k_msm_digits / k_msm_s1_scatter   Montgomery -> canonical scalar, signed
+//                       c-bit digits of all W windows; non-zero digits are
+//                       partitioned into coarse bins (bucket >> F) -- pass 1 of a
+//                       hand-written two-level counting sort (no library sort).
+//   2. k_msm_s2_*       (msm_sort.hip) each coarse bin -> its buckets: sorted
+//                       (bucket, point index | sign << 31) entries and the bucket
+//                       start offsets, written directly.
+//   3. k_msm_accum_seg  load-balanced slices of K sorted entries per thread:
 //                       lazily reduced XYZZ mixed adds of the gathered points
 //                       (sign applied on load); buckets cut by slice edges go to
 //                       part_first / part_last and are merged by k_msm_fixup
 //                       (k_msm_fix_tree + k_msm_fixup_long for spans > FIX_SERIAL).
-//   5. k_msm_seg        bucket reduction level 1: running sums over segments of
+//   4. k_msm_seg        bucket reduction level 1: running sums over segments of
 //                       L buckets;  k_msm_bitsum: LDS bit-sum trees up to one node
 //                       per window;  k_msm_export: nodes -> gnark words.
-//   6. host: Horner over the window / bit-position nodes, XYZZ -> Jacobian.
+//   5. host: Horner over the window / bit-position nodes, XYZZ -> Jacobian.
 // With a precomputed point set (MsmPrecomp) every window shares one bucket set
-// and steps 5-6 run once.
+// and steps 4-5 run once.
 //
 // Exact group arithmetic: the result is independent of summation order.
 #include "curves.hpp"
@@ -48,69 +49,71 @@ GM_DEV uint32_t window_bits(const FeG<Fr>& k, uint32_t bit, uint32_t mask) {
   return (uint32_t)(v >> sh) & mask;
 }
 
-// Decoding of the sorted (key, value) entries.  Window-major plans keep the
-// global bucket index w*nb + |d|-1 in the key.  Digit-major plans (W <= 16,
-// n < 2^27, see msm_plan) sort by |d|-1 alone -- c bits instead of
-// c + log2(W), one radix pass fewer at c = 16 -- and carry the window in value
-// bits 27..30: the sort is stable and its input window-major, so equal digits
-// stay ordered by window and b = (|d|-1) * W + w is ascending, i.e. the entries
-// are grouped by bucket in digit-major bucket order.  slot() maps b back to the
-// window-major bucket storage the reduction reads.
-struct KeyFmt {
-  uint32_t W = 0;  // 0: window-major keys; else digit-major with W windows
-  uint32_t nb = 0;
-  GM_HD uint32_t key(uint32_t k, uint32_t v) const {
-    return W ? (k >= nb ? W * nb : k * W + ((v >> 27) & 15u)) : k;
-  }
-  GM_HD uint32_t idx(uint32_t v) const { return v & (W ? 0x07ffffffu : 0x7fffffffu); }
-  GM_HD uint32_t slot(uint32_t b) const { return W ? (b % W) * nb + b / W : b; }
-};
-
 // gnark Montgomery fr.Element -> canonical integer as packed u32 words
 template <class Fr>
 GM_DEV FeG<Fr> load_scalar_canonical(const uint32_t* __restrict__ s, uint32_t i) {
   return fe_pack(fe_gnark_to_canonical(fe_load_g<Fr>(s, i)));
 }
 
-// Digit keys for a radix sort: key = global bucket index w*nb + |d|-1 (or the
-// sentinel `total` for a zero digit, which sorts past every bucket), value =
-// point index | sign << 31.  Window-major: entry (w, i) at w*n + i.
-// Precomputed (shared-bucket) layout: key = |d|-1 (sentinel nb) for every
-// window, value = index of the shifted copy, w*stride + i.
+// Plain layout: bucket b = w*nb + |d|-1 (window-major), entry value = point
+// index | sign << 31.  Precomputed (shared-bucket) layout: b = |d|-1 for every
+// window, value = w*stride + i (the shifted copy) | sign << 31.
+struct DigitGeom {
+  uint32_t n, c, W, nb, shared_stride, F;  // F: fine bits of the sort (coarse bin = b >> F)
+};
+
+// ---------------------------------------------------------------------------
+// Bucket sort of the digits: a two-level counting sort written for this job.
+// Order inside a bucket is irrelevant (group addition is exact), so no pass has
+// to be stable, and zero digits are dropped at the source.
+//   k_msm_digits     (here, per scalar field) one thread per point: the W
+//                    signed digits, stored window-major (coalesced) as
+//                    dig[w*n + i] = (|d|-1) | sign << 31 (~0: zero digit), and
+//                    the coarse histogram (bin H = bucket >> F; LDS, then one
+//                    global atomic per bin per block)
+//   msm_sort.hip     k_msm_s1_scan: coarse bases; k_msm_s1_scatter: one block
+//                    per (window, 8K points) partitions those digits into the
+//                    coarse bins (a plain-layout block only touches its own
+//                    window's bins, so its write runs are long); pass 2 sorts
+//                    every coarse bin into its 2^F buckets and writes the
+//                    sorted keys / values and the bucket offsets directly.
+// ---------------------------------------------------------------------------
+constexpr uint32_t DG_THREADS = 1024, DG_PPT = 4;
+
 template <class Fr>
-__global__ void __launch_bounds__(256) k_msm_keys(const uint32_t* __restrict__ scalars, uint32_t n,
-                                                  uint32_t c, uint32_t W, uint32_t shared_stride,
-                                                  uint32_t dmajor, uint32_t* __restrict__ keys,
-                                                  uint32_t* __restrict__ vals) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const FeG<Fr> k = load_scalar_canonical<Fr>(scalars, i);
-  const uint32_t nb = 1u << (c - 1), mask = (1u << c) - 1, total = W * nb;
-  uint32_t carry = 0;
-  for (uint32_t w = 0; w < W; w++) {
-    const uint32_t raw = window_bits(k, w * c, mask) + carry;
-    uint32_t d, neg;
-    if (raw > nb) {
-      d = (1u << c) - raw;
-      carry = 1;
-      neg = 1;
-    } else {
-      d = raw;
-      carry = 0;
-      neg = 0;
-    }
-    const size_t e = (size_t)w * n + i;
-    if (shared_stride) {
-      keys[e] = d ? d - 1 : nb;
-      vals[e] = (w * shared_stride + i) | (neg << 31);
-    } else if (dmajor) {
-      keys[e] = d ? d - 1 : nb;
-      vals[e] = i | (w << 27) | (neg << 31);
-    } else {
-      keys[e] = d ? w * nb + d - 1 : total;
-      vals[e] = i | (neg << 31);
+__global__ void __launch_bounds__(1024) k_msm_digits(const uint32_t* __restrict__ scalars, DigitGeom g,
+                                                     uint32_t NC, uint32_t* __restrict__ dig,
+                                                     uint32_t* __restrict__ ccount) {
+  extern __shared__ uint32_t dg_lds[];
+  const uint32_t t = threadIdx.x;
+  for (uint32_t q = t; q < NC; q += DG_THREADS) dg_lds[q] = 0;
+  __syncthreads();
+  const uint32_t base = blockIdx.x * DG_THREADS * DG_PPT;
+  for (uint32_t r = 0; r < DG_PPT; r++) {
+    const uint32_t i = base + r * DG_THREADS + t;
+    if (i >= g.n) break;
+    const FeG<Fr> k = load_scalar_canonical<Fr>(scalars, i);
+    const uint32_t mask = (1u << g.c) - 1;
+    uint32_t carry = 0;
+    for (uint32_t w = 0; w < g.W; w++) {
+      const uint32_t raw = window_bits(k, w * g.c, mask) + carry;
+      uint32_t d, neg;
+      if (raw > g.nb) {
+        d = (1u << g.c) - raw;
+        carry = 1;
+        neg = 1;
+      } else {
+        d = raw;
+        carry = 0;
+        neg = 0;
+      }
+      dig[(size_t)w * g.n + i] = d ? (d - 1) | (neg << 31) : 0xffffffffu;
+      if (d) atomicAdd(&dg_lds[(g.shared_stride ? d - 1 : w * g.nb + d - 1) >> g.F], 1u);
     }
   }
+  __syncthreads();
+  for (uint32_t q = t; q < NC; q += DG_THREADS)
+    if (dg_lds[q]) atomicAdd(&ccount[q], dg_lds[q]);
 }
 
 // ---------------------------------------------------------------------------
@@ -209,11 +212,11 @@ template <class F>
 GM_DEV void accum_emit(uint32_t b, const XYZZ<F>& acc_raw, bool is_first, bool is_last, uint32_t start,
                        uint32_t end, uint32_t t, const uint32_t* __restrict__ offsets,
                        XYZZ<F>* __restrict__ buckets, XYZZ<F>* __restrict__ part_first,
-                       XYZZ<F>* __restrict__ part_last, KeyFmt fmt) {
+                       XYZZ<F>* __restrict__ part_last) {
   const XYZZ<F> acc = LazyAcc<F>::canon(acc_raw);
   const uint32_t bs = offsets[b], be = offsets[b + 1];
   if (bs >= start && be <= end) {
-    buckets[fmt.slot(b)] = acc;
+    buckets[b] = acc;
   } else {
     if (is_first) part_first[t] = acc;
     if (is_last) part_last[t] = acc;
@@ -228,17 +231,17 @@ GM_DEV void accum_seg_body(const uint32_t* __restrict__ points, uint32_t n,
                                                        uint32_t K, XYZZ<F>* __restrict__ buckets,
                                                        XYZZ<F>* __restrict__ part_first,
                                                        XYZZ<F>* __restrict__ part_last,
-                                                       uint32_t* __restrict__ err, KeyFmt fmt) {
+                                                       uint32_t* __restrict__ err) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t Mv = offsets[total];  // valid (non-zero-digit) entries
   const uint32_t start = t * K;
   if (start >= Mv) return;
   const uint32_t end = min(start + K, Mv);
   uint32_t v = vals[start];
-  uint32_t cur = fmt.key(keys[start], v);
+  uint32_t cur = keys[start];
   bool first = true;
   XYZZ<F> acc = xyzz_inf<F>();
-  uint32_t idx = fmt.idx(v);
+  uint32_t idx = v & 0x7fffffffu;
   if (idx >= n) {
     atomicOr(err, 2u);
     return;
@@ -246,13 +249,13 @@ GM_DEV void accum_seg_body(const uint32_t* __restrict__ points, uint32_t n,
   constexpr int PW = 2 * Coord<F>::WORDS;  // u32 words per packed point
   PackedPt<PW> P = load_packed_pt<PW>(points + (size_t)idx * PW);
   for (uint32_t q = start; q < end; q++) {
-    const uint32_t k = fmt.key(keys[q], v);
+    const uint32_t k = keys[q];
     // prefetch the next point's words while this add runs
     uint32_t vn = 0;
     PackedPt<PW> Pn;
     if (PREFETCH && q + 1 < end) {
       vn = vals[q + 1];
-      const uint32_t in = fmt.idx(vn);
+      const uint32_t in = vn & 0x7fffffffu;
       if (in >= n) {
         atomicOr(err, 2u);
         return;
@@ -260,12 +263,12 @@ GM_DEV void accum_seg_body(const uint32_t* __restrict__ points, uint32_t n,
       Pn = load_packed_pt<PW>(points + (size_t)in * PW);
     }
     if (k != cur) {
-      accum_emit(cur, acc, first, false, start, end, t, offsets, buckets, part_first, part_last, fmt);
+      accum_emit(cur, acc, first, false, start, end, t, offsets, buckets, part_first, part_last);
       first = false;
       acc = xyzz_inf<F>();
       cur = k;
     }
-    if (!PREFETCH) P = load_packed_pt<PW>(points + (size_t)fmt.idx(v) * PW);
+    if (!PREFETCH) P = load_packed_pt<PW>(points + (size_t)(v & 0x7fffffffu) * PW);
     Affine<F> A = load_affine_packed<F>(P.w);
     if (v >> 31) A.y = fe_neg(A.y);
     LazyAcc<F>::add(acc, A);
@@ -274,13 +277,13 @@ GM_DEV void accum_seg_body(const uint32_t* __restrict__ points, uint32_t n,
       P = Pn;
     } else if (q + 1 < end) {
       v = vals[q + 1];
-      if (fmt.idx(v) >= n) {
+      if ((v & 0x7fffffffu) >= n) {
         atomicOr(err, 2u);
         return;
       }
     }
   }
-  accum_emit(cur, acc, first, true, start, end, t, offsets, buckets, part_first, part_last, fmt);
+  accum_emit(cur, acc, first, true, start, end, t, offsets, buckets, part_first, part_last);
 }
 
 
@@ -292,9 +295,8 @@ __global__ void __launch_bounds__(128) k_msm_accum_seg(const uint32_t* __restric
                                                        const uint32_t* __restrict__ offsets, uint32_t total,
                                                        uint32_t K, XYZZ<F>* __restrict__ buckets,
                                                        XYZZ<F>* __restrict__ part_first,
-                                                       XYZZ<F>* __restrict__ part_last, uint32_t* __restrict__ err,
-                                                       KeyFmt fmt) {
-  accum_seg_body<F, true>(points, n, keys, vals, offsets, total, K, buckets, part_first, part_last, err, fmt);
+                                                       XYZZ<F>* __restrict__ part_last, uint32_t* __restrict__ err) {
+  accum_seg_body<F, true>(points, n, keys, vals, offsets, total, K, buckets, part_first, part_last, err);
 }
 
 // G2 (Fp2 coordinates): a mixed add keeps ~330 registers live, i.e. one wave per
@@ -305,8 +307,8 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2)))
 k_msm_accum_seg_g2(const uint32_t* __restrict__ points, uint32_t n, const uint32_t* __restrict__ keys,
                    const uint32_t* __restrict__ vals, const uint32_t* __restrict__ offsets, uint32_t total,
                    uint32_t K, XYZZ<F>* __restrict__ buckets, XYZZ<F>* __restrict__ part_first,
-                   XYZZ<F>* __restrict__ part_last, uint32_t* __restrict__ err, KeyFmt fmt) {
-  accum_seg_body<F, false>(points, n, keys, vals, offsets, total, K, buckets, part_first, part_last, err, fmt);
+                   XYZZ<F>* __restrict__ part_last, uint32_t* __restrict__ err) {
+  accum_seg_body<F, false>(points, n, keys, vals, offsets, total, K, buckets, part_first, part_last, err);
 }
 
 // Merge the partial sums of buckets cut by slice edges.  Bucket b spans slices
@@ -322,7 +324,7 @@ __global__ void __launch_bounds__(128) k_msm_fixup(const uint32_t* __restrict__ 
                                                    uint32_t K, XYZZ<F>* __restrict__ buckets,
                                                    const XYZZ<F>* __restrict__ part_first,
                                                    const XYZZ<F>* __restrict__ part_last,
-                                                   uint32_t* __restrict__ maxspan, KeyFmt fmt) {
+                                                   uint32_t* __restrict__ maxspan) {
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= total) return;
   const uint32_t bs = offsets[b], be = offsets[b + 1];
@@ -335,19 +337,18 @@ __global__ void __launch_bounds__(128) k_msm_fixup(const uint32_t* __restrict__ 
   }
   XYZZ<F> acc = part_last[t0];
   for (uint32_t t = t0 + 1; t <= t1; t++) acc = xyzz_add(acc, part_first[t]);
-  buckets[fmt.slot(b)] = acc;
+  buckets[b] = acc;
 }
 
 // One level d of the pairwise tree over part_first[t0+1 .. t1] of every long span.
 template <class F>
 __global__ void __launch_bounds__(128) k_msm_fix_tree(const uint32_t* __restrict__ keys,
-                                                      const uint32_t* __restrict__ vals,
                                                       const uint32_t* __restrict__ offsets, uint32_t total,
                                                       uint32_t K, uint32_t nslices, uint32_t d,
-                                                      XYZZ<F>* __restrict__ part_first, KeyFmt fmt) {
+                                                      XYZZ<F>* __restrict__ part_first) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nslices || (size_t)t * K >= offsets[total]) return;
-  const uint32_t b = fmt.W ? fmt.key(keys[(size_t)t * K], vals[(size_t)t * K]) : keys[(size_t)t * K];
+  const uint32_t b = keys[(size_t)t * K];
   const uint32_t t0 = offsets[b] / K, t1 = (offsets[b + 1] - 1) / K;
   if (t1 - t0 <= FIX_SERIAL || t <= t0) return;
   const uint32_t rel = t - (t0 + 1), len = t1 - t0, step = 1u << d;
@@ -359,14 +360,14 @@ template <class F>
 __global__ void __launch_bounds__(128) k_msm_fixup_long(const uint32_t* __restrict__ offsets, uint32_t total,
                                                         uint32_t K, XYZZ<F>* __restrict__ buckets,
                                                         const XYZZ<F>* __restrict__ part_first,
-                                                        const XYZZ<F>* __restrict__ part_last, KeyFmt fmt) {
+                                                        const XYZZ<F>* __restrict__ part_last) {
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= total) return;
   const uint32_t bs = offsets[b], be = offsets[b + 1];
   if (be == bs) return;
   const uint32_t t0 = bs / K, t1 = (be - 1) / K;
   if (t1 - t0 <= FIX_SERIAL) return;
-  buckets[fmt.slot(b)] = xyzz_add(part_last[t0], part_first[t0 + 1]);
+  buckets[b] = xyzz_add(part_last[t0], part_first[t0 + 1]);
 }
 
 // ---------------------------------------------------------------------------
@@ -464,60 +465,6 @@ __global__ void __launch_bounds__(128) k_msm_export(const XYZZ<F>* __restrict__ 
   Coord<F>::store_gnark(o + 3 * Coord<F>::WORDS, r.zzz);
 }
 
-// offsets[b] = first sorted position with key >= b (lower bound), b in [0, total]:
-// window-major keys, one binary search per bucket.
-static __global__ void __launch_bounds__(256) k_msm_lower_bound(const uint32_t* __restrict__ keys, uint32_t M,
-                                                         uint32_t total, uint32_t* __restrict__ offsets) {
-  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b > total) return;
-  uint32_t lo = 0, hi = M;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (keys[mid] < b) lo = mid + 1;
-    else hi = mid;
-  }
-  offsets[b] = lo;
-}
-
-// Digit-major keys (two loads per probe make a binary search per bucket ~2x
-// slower): the same offsets from one linear pass -- entry q (q <= M) owns the
-// buckets b with key(q-1) < b <= key(q) (key(-1) = -1, key(M) = total).  Gaps of
-// at most BOUNDS_GAP empty buckets are written by the entry that ends them; for
-// a longer gap (sparse keys: zero-heavy or constant scalars) the entry writes
-// only its own bucket and k_msm_bounds_fill binary-searches the rest, so no lane
-// loops over more than BOUNDS_GAP buckets.  `offsets` is preset to ~0.
-constexpr uint32_t BOUNDS_GAP = 32;
-static __global__ void __launch_bounds__(256) k_msm_bounds(const uint32_t* __restrict__ keys,
-                                                    const uint32_t* __restrict__ vals, uint32_t M, uint32_t total,
-                                                    uint32_t* __restrict__ offsets, KeyFmt fmt) {
-  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q > M) return;
-  const uint32_t hi = q == M ? total : min(fmt.W ? fmt.key(keys[q], vals[q]) : keys[q], total);
-  const uint32_t lo = q == 0 ? 0u : (fmt.W ? fmt.key(keys[q - 1], vals[q - 1]) : keys[q - 1]) + 1;
-  if (hi < lo) return;
-  if (hi - lo > BOUNDS_GAP) {
-    offsets[hi] = q;
-    return;
-  }
-  for (uint32_t b = lo; b <= hi; b++) offsets[b] = q;
-}
-
-// Buckets k_msm_bounds left unset (~0): lower bound by binary search.
-static __global__ void __launch_bounds__(256) k_msm_bounds_fill(const uint32_t* __restrict__ keys,
-                                                         const uint32_t* __restrict__ vals, uint32_t M,
-                                                         uint32_t total, uint32_t* __restrict__ offsets,
-                                                         KeyFmt fmt) {
-  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b > total || offsets[b] != 0xffffffffu) return;
-  uint32_t lo = 0, hi = M;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (fmt.key(keys[mid], vals[mid]) < b) lo = mid + 1;
-    else hi = mid;
-  }
-  offsets[b] = lo;
-}
-
 // ---------------------------------------------------------------------------
 // host driver
 // ---------------------------------------------------------------------------
@@ -568,64 +515,58 @@ int msm_plan(gm_ctx* ctx, Arena& arena, const void* scalars_dev, size_t n, const
   plan.Wred = shared ? 1 : W;
   plan.total = plan.Wred * plan.nb;
   plan.npts = shared ? (size_t)W * pre->stride : n;
-  // digit-major keys (KeyFmt) when they save a radix pass: c bits instead of
-  // bits(W * nb); needs the window in 4 value bits and the index in 27
-  {
-    int wm_bits = 1;
-    while ((1ull << wm_bits) <= plan.total) wm_bits++;
-    static const char* dm = getenv("GM_MSM_DMAJOR");  // 0 = off (A/B)
-    const bool allow = !dm || atoi(dm) != 0;
-    if (allow && !shared && W <= 16 && n < (size_t(1) << 27) && (c + 7) / 8 < (uint32_t)(wm_bits + 7) / 8)
-      plan.dW = W;
-  }
-  const size_t M = (size_t)W * n;
+  const size_t M = (size_t)W * n;  // upper bound on the entries: zero digits are dropped
   plan.M = M;
   if (M >= (size_t(1) << 31)) {
     set_error("msm: n * windows must be < 2^31");
     return GM_ERR_INVALID;
   }
-  int rc;
-  DevBuf keys_in, vals_in, keys_out, vals_out, offsets;
-  if ((rc = keys_in.alloc(arena, sizeof(uint32_t) * M)) || (rc = vals_in.alloc(arena, sizeof(uint32_t) * M)) ||
-      (rc = keys_out.alloc(arena, sizeof(uint32_t) * M)) || (rc = vals_out.alloc(arena, sizeof(uint32_t) * M)) ||
-      (rc = offsets.alloc(arena, sizeof(uint32_t) * (plan.total + 1))))
-    return rc;
-  {
-    ProfScope ps(ctx, "msm_keys");
-    hipLaunchKernelGGL(k_msm_keys<typename C::Fr>, dim3(blocks_for(n, 256)), dim3(256), 0, st,
-                       reinterpret_cast<const uint32_t*>(scalars_dev), (uint32_t)n, c, W,
-                       shared ? (uint32_t)pre->stride : 0u, plan.dW ? 1u : 0u, keys_in.as<uint32_t>(),
-                       vals_in.as<uint32_t>());
+  // Sort geometry: ~2K entries per coarse bin for uniform digits (pass 2 stages a
+  // bin of up to S2_STAGE entries in LDS; the narrow top window's bins are ~2x
+  // fuller), at most 8192 coarse bins and 2^13 fine bins per coarse bin.
+  SortGeom sg;
+  sg.T = plan.total;
+  sg.M = M;
+  sg.F = 4;
+  while (sg.F < 13 && (double)M * std::ldexp(1.0, (int)sg.F + 1) <= 2048.0 * sg.T) sg.F++;
+  while (sg.F < 13 && ((sg.T + (1u << sg.F) - 1) >> sg.F) > 8192) sg.F++;
+  sg.NC = (sg.T + (1u << sg.F) - 1) >> sg.F;
+  if (sg.NC > 8192) {
+    set_error("msm: too many buckets for the sort");
+    return GM_ERR_INVALID;
   }
-  GM_HIP(hipGetLastError());
-  // sort key range: bucket indices + the zero-digit sentinel (total), or for
-  // digit-major keys |d|-1 + the sentinel nb
-  const uint64_t key_max = plan.dW ? plan.nb : plan.total;
-  int end_bit = 1;
-  while ((1ull << end_bit) <= key_max) end_bit++;
+  int rc;
+  DevBuf dig, tmp, keys_out, vals_out, offsets, ccount, cbase, ccursor, pbase, fcount;
+  if ((rc = dig.alloc(arena, sizeof(uint32_t) * M)) || (rc = tmp.alloc(arena, sizeof(uint64_t) * M)) ||
+      (rc = keys_out.alloc(arena, sizeof(uint32_t) * M)) || (rc = vals_out.alloc(arena, sizeof(uint32_t) * M)) ||
+      (rc = offsets.alloc(arena, sizeof(uint32_t) * ((size_t)plan.total + 1))) ||
+      (rc = ccount.alloc(arena, sizeof(uint32_t) * sg.NC)) || (rc = cbase.alloc(arena, sizeof(uint32_t) * (sg.NC + 1))) ||
+      (rc = ccursor.alloc(arena, sizeof(uint32_t) * sg.NC)) || (rc = pbase.alloc(arena, sizeof(uint32_t) * (sg.NC + 1))) ||
+      (rc = fcount.alloc(arena, sizeof(uint32_t) * (size_t)plan.total)))
+    return rc;
+  DigitGeom g;
+  g.n = (uint32_t)n;
+  g.c = c;
+  g.W = W;
+  g.nb = plan.nb;
+  g.shared_stride = shared ? (uint32_t)pre->stride : 0u;
+  g.F = sg.F;
+  {
+    ProfScope ps(ctx, "msm_digits");
+    GM_HIP(hipMemsetAsync(ccount.p, 0, sizeof(uint32_t) * sg.NC, st));
+    hipLaunchKernelGGL(k_msm_digits<typename C::Fr>, dim3(blocks_for(n, DG_THREADS * DG_PPT)), dim3(DG_THREADS),
+                       sizeof(uint32_t) * sg.NC, st, reinterpret_cast<const uint32_t*>(scalars_dev), g, sg.NC,
+                       dig.as<uint32_t>(), ccount.as<uint32_t>());
+    GM_HIP(hipGetLastError());
+  }
   {
     ProfScope ps(ctx, "msm_sort");
-    if ((rc = msm_sort_pairs(ctx, arena, keys_in.as<uint32_t>(), keys_out.as<uint32_t>(), vals_in.as<uint32_t>(),
-                             vals_out.as<uint32_t>(), M, end_bit)))
+    if ((rc = msm_sort_digits(ctx, sg, n, W, plan.nb, g.shared_stride, dig.as<uint32_t>(), ccount.as<uint32_t>(),
+                              cbase.as<uint32_t>(), ccursor.as<uint32_t>(), pbase.as<uint32_t>(),
+                              tmp.as<uint64_t>(), fcount.as<uint32_t>(), keys_out.as<uint32_t>(),
+                              vals_out.as<uint32_t>(), offsets.as<uint32_t>())))
       return rc;
   }
-  {
-    ProfScope ps(ctx, "msm_offsets");
-    KeyFmt fmt;
-    fmt.W = plan.dW;
-    fmt.nb = plan.nb;
-    if (fmt.W) {
-      GM_HIP(hipMemsetAsync(offsets.p, 0xff, sizeof(uint32_t) * (plan.total + 1), st));
-      hipLaunchKernelGGL(k_msm_bounds, dim3(blocks_for(M + 1, 256)), dim3(256), 0, st, keys_out.as<uint32_t>(),
-                         vals_out.as<uint32_t>(), (uint32_t)M, plan.total, offsets.as<uint32_t>(), fmt);
-      hipLaunchKernelGGL(k_msm_bounds_fill, dim3(blocks_for((size_t)plan.total + 1, 256)), dim3(256), 0, st,
-                         keys_out.as<uint32_t>(), vals_out.as<uint32_t>(), (uint32_t)M, plan.total,
-                         offsets.as<uint32_t>(), fmt);
-    } else
-      hipLaunchKernelGGL(k_msm_lower_bound, dim3(blocks_for((size_t)plan.total + 1, 256)), dim3(256), 0, st,
-                         keys_out.as<uint32_t>(), (uint32_t)M, plan.total, offsets.as<uint32_t>());
-  }
-  GM_HIP(hipGetLastError());
   plan.keys = keys_out.as<uint32_t>();
   plan.vals = vals_out.as<uint32_t>();
   plan.offsets = offsets.as<uint32_t>();
@@ -664,9 +605,6 @@ int msm_run(gm_ctx* ctx, const MsmPlan& plan, const void* points_internal,
   if ((rc = wsum.alloc(arena, sizeof(uint32_t) * 4 * WORDS * Wr * (2 + c)))) return rc;
   const uint32_t* pts_internal = reinterpret_cast<const uint32_t*>(points_internal);
   const uint32_t* offsets = plan.offsets;
-  KeyFmt fmt;
-  fmt.W = plan.dW;
-  fmt.nb = nb;
   DevBuf pfirst, plast;
   {
     const uint32_t K = ctx->msm_slice ? (uint32_t)ctx->msm_slice : 64u;
@@ -683,10 +621,10 @@ int msm_run(gm_ctx* ctx, const MsmPlan& plan, const void* points_internal,
     auto accum = noprefetch ? k_msm_accum_seg_g2<DF> : k_msm_accum_seg<DF>;
     hipLaunchKernelGGL(accum, dim3(blocks_for(nslices, 128)), dim3(128), 0, st, pts_internal,
                        (uint32_t)plan.npts, plan.keys, plan.vals, offsets, total, K, buckets.as<XYZZ<DF>>(),
-                       pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>(), errw.as<uint32_t>(), fmt);
+                       pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>(), errw.as<uint32_t>());
     hipLaunchKernelGGL(k_msm_fixup<DF>, dim3(blocks_for(total, 128)), dim3(128), 0, st, offsets, total, K,
                        buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>(),
-                       errw.as<uint32_t>() + 1, fmt);
+                       errw.as<uint32_t>() + 1);
   }
   // Bucket reduction, launched speculatively: buckets spanning more than
   // FIX_SERIAL slices (skewed scalars) are only known once errw[1] (max span)
@@ -757,9 +695,9 @@ int msm_run(gm_ctx* ctx, const MsmPlan& plan, const void* points_internal,
         const size_t nslices = (M + K - 1) / K;
         for (uint32_t d = 0; (1u << d) < ms; d++)
           hipLaunchKernelGGL(k_msm_fix_tree<DF>, dim3(blocks_for(nslices, 128)), dim3(128), 0, st, plan.keys,
-                             plan.vals, offsets, total, K, (uint32_t)nslices, d, pfirst.as<XYZZ<DF>>(), fmt);
+                             offsets, total, K, (uint32_t)nslices, d, pfirst.as<XYZZ<DF>>());
         hipLaunchKernelGGL(k_msm_fixup_long<DF>, dim3(blocks_for(total, 128)), dim3(128), 0, st, offsets, total,
-                           K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>(), fmt);
+                           K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>());
         GM_HIP(hipMemsetAsync(errw.as<uint32_t>() + 1, 0, 4, st));  // long spans resolved
       }
     }
@@ -773,9 +711,9 @@ int msm_run(gm_ctx* ctx, const MsmPlan& plan, const void* points_internal,
     const size_t nslices = (M + K - 1) / K;
     for (uint32_t d = 0; (1u << d) < maxspan; d++)
       hipLaunchKernelGGL(k_msm_fix_tree<DF>, dim3(blocks_for(nslices, 128)), dim3(128), 0, st, plan.keys,
-                         plan.vals, offsets, total, K, (uint32_t)nslices, d, pfirst.as<XYZZ<DF>>(), fmt);
+                         offsets, total, K, (uint32_t)nslices, d, pfirst.as<XYZZ<DF>>());
     hipLaunchKernelGGL(k_msm_fixup_long<DF>, dim3(blocks_for(total, 128)), dim3(128), 0, st, offsets, total, K,
-                       buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>(), fmt);
+                       buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>());
     if ((rc = reduce()) || (rc = readback())) return rc;
     memcpy(&herr, stage, 4);
   }

@@ -45,7 +45,7 @@ def test_msm_small_vs_pyref(gm_ctx, cname, g2):
     pb = b"".join(pyref.encode_point(c, p, g2) for p in pts)
     S = gm_ctx.copy_to_device(sb)
     P = gm_ctx.copy_points_to_device(cname, pb, g2)
-    for window in (0, 4, 9, 16):  # 16: digit-major sort keys (KeyFmt)
+    for window in (0, 4, 9, 16):  # each window size gives a different sort geometry (F, NC)
         gm_ctx.set_msm_window(window)
         jac, aff = gm_ctx.msm(cname, S, P, n, g2)
         assert pyref.decode_point(c, aff, g2) == exp, (cname, g2, window)
@@ -54,7 +54,7 @@ def test_msm_small_vs_pyref(gm_ctx, cname, g2):
     P.free()
 
 
-@pytest.mark.parametrize("window", [0, 16])  # 16: digit-major plan (KeyFmt)
+@pytest.mark.parametrize("window", [0, 16])
 @pytest.mark.parametrize("cname,g2", CASES)
 def test_msm_empty_and_single(gm_ctx, cname, g2, window):
     import gnark_mi355x as gm
@@ -77,9 +77,9 @@ def test_msm_empty_and_single(gm_ctx, cname, g2, window):
 @pytest.mark.parametrize("value", [0, 1, "r-1"])
 @pytest.mark.parametrize("cname,g2", [("bn254", False), ("bls12377", True)])
 def test_msm_constant_scalars_c16(gm_ctx, oracle, cname, g2, value):
-    """All scalars equal at c = 16 (digit-major offsets, msm_plan): 0 (every
-    entry is a zero digit -- all buckets empty), 1 (one bucket, all others empty)
-    and r-1 (every window's top digit)."""
+    """All scalars equal at c = 16: 0 (every digit is zero -- nothing enters the
+    sort, all buckets empty), 1 (one bucket, all others empty) and r-1 (every
+    window's top digit)."""
     import gnark_mi355x as gm
     c = pyref.CURVES[cname]
     n = (1 << 14) + 3
@@ -321,16 +321,17 @@ def test_msm_bucket_chain_special_cases(gm_ctx, cname, g2, window):
 
 @pytest.mark.parametrize("cname,g2,logn", [("bn254", False, 14), ("bn254", True, 12),
                                            ("bls12377", False, 13), ("bls12377", True, 11)])
-def test_msm_digit_major_keys_vs_oracle(gm_ctx, oracle, cname, g2, logn):
-    """c = 16 (W = 16): the plan sorts by digit only and carries the window in
-    the value bits (KeyFmt); window-major (GM_MSM_DMAJOR semantics) must agree."""
+def test_msm_sort_geometries_vs_oracle(gm_ctx, oracle, cname, g2, logn):
+    """Window sizes 8..20 give bucket counts from 2^12 to 13 * 2^19, i.e. every
+    shape of the two-level bucket sort: one coarse bin covering all buckets
+    (F >= log2 T), ~16K entries per coarse bin, and mostly empty buckets."""
     import gnark_mi355x as gm
     n = (1 << logn) + 11
     S = gm_ctx.random_scalars(cname, n, seed=0x5EED0007 + logn)
     K = gm_ctx.random_scalars(cname, n, seed=0x5EED1007 + logn)
     P = gm_ctx.batch_mul_base(cname, g2, gm.generator(cname, g2), K, n)
     exp = oracle.msm(cname, g2, S.to_host(), P.to_host())
-    for c in (16, 15):  # 15: W = 17 windows -> window-major keys
+    for c in (16, 15, 8, 20):
         gm_ctx.set_msm_window(c)
         try:
             assert gm_ctx.msm(cname, S, P, n, g2)[1] == exp, c
@@ -338,3 +339,22 @@ def test_msm_digit_major_keys_vs_oracle(gm_ctx, oracle, cname, g2, logn):
             gm_ctx.set_msm_window(0)
     for b in (S, K, P):
         b.free()
+
+
+@pytest.mark.parametrize("value", [1, 3])
+def test_msm_split_coarse_bin(gm_ctx, oracle, value):
+    """One bucket holding 2^19 + 5 entries (> S2_BIG = 2^18): its coarse bin is
+    split into parts (k_msm_s2_scan / k_msm_s2_scatter path of the sort)."""
+    import gnark_mi355x as gm
+    cname = "bn254"
+    c = pyref.CURVES[cname]
+    n = (1 << 19) + 5
+    sb = pyref.encode_fr(c, value) * n
+    K = gm_ctx.random_scalars(cname, n, seed=0x5117)
+    P = gm_ctx.batch_mul_base(cname, False, gm.generator(cname, False), K, n)
+    S = gm_ctx.copy_to_device(sb)
+    try:
+        assert gm_ctx.msm(cname, S, P, n, False)[1] == oracle.msm(cname, False, sb, P.to_host())
+    finally:
+        for b in (S, K, P):
+            b.free()
