@@ -26,24 +26,12 @@
 #include "curves.hpp"
 #include "msm.hpp"
 #include "ntt.hpp"
+#include "groth16.hpp"
 #include "runtime.hpp"
 
 using namespace gm;
 
-struct gm_g16_pk {
-  int curve;
-  size_t n, nb_wires, nb_public, nbA, nbB, nbK;
-  void *A = nullptr, *B = nullptr, *Z = nullptr, *K = nullptr, *B2 = nullptr;  // device point arrays
-  void *idxA = nullptr, *idxB = nullptr, *idxK = nullptr;  // device compaction maps (wire - wlo)
-  size_t zlo = 0, nbZ = 0;      // this key's slice of h / pk.G1.Z (whole key: 0, n-1)
-  size_t wlo = 0, whi = 0;      // wires the maps address: [wlo, whi) (whole key: 0, nb_wires)
-  bool precomp = false;         // GM_PK_PRECOMPUTE: fixed-base window copies
-  MsmPrecomp preA, preB, preZ, preK;  // layouts (B and B2 share preB)
-  std::vector<uint8_t> alpha, beta, delta, beta2, delta2;  // host affine
-};
-
 namespace gm {
-namespace {
 
 int check_curve_id(int curve) {
   if (curve != GM_BN254 && curve != GM_BLS12_377) {
@@ -53,6 +41,7 @@ int check_curve_id(int curve) {
   return GM_OK;
 }
 
+namespace {
 // dst[i] = src[idx[i]] (Fr, 32 bytes) -- device-side scalar compaction
 __global__ void k_gather_fr(const uint4* __restrict__ src, const uint32_t* __restrict__ idx, size_t n,
                             uint4* __restrict__ dst) {
@@ -81,10 +70,7 @@ void shard_weighted(size_t n, const std::vector<double>& w, int k, size_t* lo, s
   *hi = k + 1 == (int)w.size() ? n : (size_t)((double)n * (before + w[k]) / tot);
 }
 
-struct Ranges {
-  size_t loA, hiA, loB, hiB, loK, hiK, loZ, hiZ;
-  bool rebase;  // index maps relative to the lowest wire they address (gm_multi keys)
-};
+}  // namespace
 
 size_t internal_point_bytes(int curve, bool g2) {
   if (curve == GM_BN254)
@@ -98,12 +84,28 @@ void pk_release(gm_g16_pk* pk) {
   delete pk;
 }
 
+int prepare_points_into(gm_ctx* ctx, int curve, bool g2, const void* gnark_dev, size_t count,
+                        const MsmPrecomp* pre, void* dst) {
+  if (pre) {
+    if (curve == GM_BN254)
+      return g2 ? msm_precompute_points<CurveBN254, true>(ctx, gnark_dev, count, *pre, dst)
+                : msm_precompute_points<CurveBN254, false>(ctx, gnark_dev, count, *pre, dst);
+    return g2 ? msm_precompute_points<CurveBLS12377, true>(ctx, gnark_dev, count, *pre, dst)
+              : msm_precompute_points<CurveBLS12377, false>(ctx, gnark_dev, count, *pre, dst);
+  }
+  if (curve == GM_BN254)
+    return g2 ? msm_prepare_points<CurveBN254, true>(ctx, gnark_dev, count, dst)
+              : msm_prepare_points<CurveBN254, false>(ctx, gnark_dev, count, dst);
+  return g2 ? msm_prepare_points<CurveBLS12377, true>(ctx, gnark_dev, count, dst)
+            : msm_prepare_points<CurveBLS12377, false>(ctx, gnark_dev, count, dst);
+}
+
 // Uploads the [lo, hi) slices of the key's point arrays (h's pointers address
-// the first point of each slice) and the matching slices of the compaction maps
-// (setupDevicePointers, icicle.go:31-130; the maps replace icicle.go:231-278's
-// host filtering, prove.go:157-178 / 243-245).
+// the first point of each slice, or `src` fetches them) and the matching slices
+// of the compaction maps (setupDevicePointers, icicle.go:31-130; the maps
+// replace icicle.go:231-278's host filtering, prove.go:157-178 / 243-245).
 int pk_upload_ranges(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsigned flags, const Ranges& rg,
-                     gm_g16_pk** out) {
+                     gm_g16_pk** out, const PointSource* src) {
   auto* pk = new gm_g16_pk();
   pk->curve = curve;
   pk->n = h->domain_size;
@@ -144,44 +146,31 @@ int pk_upload_ranges(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsigned f
   };
   // gnark-layout points -> device-internal layout, once (plus the W-1
   // window-shifted copies with GM_PK_PRECOMPUTE, msm_precompute_points)
-  auto up_pts = [&](const void* src, size_t count, bool g2, const MsmPrecomp& pre, void** dst) -> int {
+  auto up_pts = [&](int which, const void* hsrc, size_t count, bool g2, const MsmPrecomp& pre, void** dst) -> int {
+    const size_t copies = pk->precomp ? pre.W : 1;
+    hipError_t e = hipMalloc(dst, internal_point_bytes(curve, g2) * (count ? count * copies : 1));
+    if (e != hipSuccess) {
+      set_error(std::string("pk upload hipMalloc: ") + hipGetErrorString(e));
+      return GM_ERR_OOM;
+    }
+    if (src) return (*src)(which, count, g2, pk->precomp ? &pre : nullptr, *dst);
     void* tmp = nullptr;
-    int r = up(src, (g2 ? g2b : g1b) * count, &tmp);
+    int r = up(hsrc, (g2 ? g2b : g1b) * count, &tmp);
     if (r) {
       if (tmp) hipFree(tmp);
       return r;
     }
-    const size_t copies = pk->precomp ? pre.W : 1;
-    hipError_t e = hipMalloc(dst, internal_point_bytes(curve, g2) * (count ? count * copies : 1));
-    if (e != hipSuccess) {
-      hipFree(tmp);
-      set_error(std::string("pk upload hipMalloc: ") + hipGetErrorString(e));
-      return GM_ERR_OOM;
-    }
-    if (pk->precomp) {
-      if (curve == GM_BN254)
-        r = g2 ? msm_precompute_points<CurveBN254, true>(ctx, tmp, count, pre, *dst)
-               : msm_precompute_points<CurveBN254, false>(ctx, tmp, count, pre, *dst);
-      else
-        r = g2 ? msm_precompute_points<CurveBLS12377, true>(ctx, tmp, count, pre, *dst)
-               : msm_precompute_points<CurveBLS12377, false>(ctx, tmp, count, pre, *dst);
-    } else if (curve == GM_BN254) {
-      r = g2 ? msm_prepare_points<CurveBN254, true>(ctx, tmp, count, *dst)
-             : msm_prepare_points<CurveBN254, false>(ctx, tmp, count, *dst);
-    } else {
-      r = g2 ? msm_prepare_points<CurveBLS12377, true>(ctx, tmp, count, *dst)
-             : msm_prepare_points<CurveBLS12377, false>(ctx, tmp, count, *dst);
-    }
+    r = prepare_points_into(ctx, curve, g2, tmp, count, pk->precomp ? &pre : nullptr, *dst);
     hipStreamSynchronize(ctx->stream);
     hipFree(tmp);
     return r;
   };
   int rc;
-  if ((rc = up_pts(h->g1_A, pk->nbA, false, pk->preA, &pk->A)) ||
-      (rc = up_pts(h->g1_B, pk->nbB, false, pk->preB, &pk->B)) ||
-      (rc = up_pts(h->g1_Z, pk->nbZ, false, pk->preZ, &pk->Z)) ||
-      (rc = up_pts(h->g1_K, pk->nbK, false, pk->preK, &pk->K)) ||
-      (rc = up_pts(h->g2_B, pk->nbB, true, pk->preB, &pk->B2)))
+  if ((rc = up_pts(PK_A, h->g1_A, pk->nbA, false, pk->preA, &pk->A)) ||
+      (rc = up_pts(PK_B, h->g1_B, pk->nbB, false, pk->preB, &pk->B)) ||
+      (rc = up_pts(PK_Z, h->g1_Z, pk->nbZ, false, pk->preZ, &pk->Z)) ||
+      (rc = up_pts(PK_K, h->g1_K, pk->nbK, false, pk->preK, &pk->K)) ||
+      (rc = up_pts(PK_B2, h->g2_B, pk->nbB, true, pk->preB, &pk->B2)))
     return fail(rc);
   // compaction maps (prove.go:157-178: drop wire i when InfinityA[i] / InfinityB[i];
   // K: the k_wires survivors of filterHeap, prove.go:243-245, or nb_public + i)
@@ -237,6 +226,8 @@ int pk_upload_ranges(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsigned f
   *out = pk;
   return GM_OK;
 }
+
+namespace {
 
 // ---------------------------------------------------------------------------
 // Sources of h (the bit-reversed computeH output, icicle.go:453-513 /
@@ -649,7 +640,7 @@ int gm_g16_pk_upload_shard(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsi
   shard_of(h->nbK, rank, world, &rg.loK, &rg.hiK);
   shard_of(h->domain_size - 1, rank, world, &rg.loZ, &rg.hiZ);
   rg.rebase = false;
-  return pk_upload_ranges(ctx, curve, h, flags, rg, out);
+  return pk_upload_ranges(ctx, curve, h, flags, rg, out, nullptr);
 }
 
 int gm_g16_pk_free(gm_ctx* ctx, gm_g16_pk* pk) {
@@ -857,7 +848,7 @@ int gm_g16_pk_upload_multi(gm_multi* m, int curve, const gm_g16_pk_host* h, unsi
       hs.g1_K = (const uint8_t*)h->g1_K + g1b * rg.loK;
       hs.g1_Z = (const uint8_t*)h->g1_Z + g1b * rg.loZ;
       hs.g2_B = (const uint8_t*)h->g2_B + g2b * rg.loB;
-      rcs[d] = pk_upload_ranges(ctx, curve, &hs, flags, rg, &mp->pk[d]);
+      rcs[d] = pk_upload_ranges(ctx, curve, &hs, flags, rg, &mp->pk[d], nullptr);
       if (rcs[d]) errs[d] = gm_last_error();
     });
   }

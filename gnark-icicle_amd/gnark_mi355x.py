@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import struct
 
 import numpy as np
 
@@ -49,6 +50,9 @@ SYMBOLS = [
     "gm_test_point_op", "gm_icicle_generate_twiddles", "gm_icicle_intt_on_device", "gm_icicle_ntt_on_device",
     "gm_icicle_poly_ops", "gm_device_count", "gm_multi_init", "gm_multi_destroy", "gm_multi_size",
     "gm_multi_context", "gm_g16_pk_upload_multi", "gm_g16_pk_free_multi", "gm_g16_prove_multi",
+    "gm_g16_pk_upload_dump", "gm_g16_pk_upload_dump_shard", "gm_g16_pk_save_cache", "gm_g16_pk_load_cache",
+    "gm_g16_stage_begin", "gm_g16_stage_put_range", "gm_g16_stage_put_indexed", "gm_g16_stage_prove",
+    "gm_g16_stage_free",
 ]
 
 
@@ -125,6 +129,15 @@ def load_library(path: str = LIB_PATH):
     L.gm_g16_pk_upload_multi.argtypes = [vp, i, vp, ctypes.c_uint, pvp]
     L.gm_g16_pk_free_multi.argtypes = [vp, vp]
     L.gm_g16_prove_multi.argtypes = [vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, vp, vp]
+    L.gm_g16_pk_upload_dump.argtypes = [vp, i, vp, i, u64, ctypes.c_uint, ctypes.POINTER(u64), pvp]
+    L.gm_g16_pk_upload_dump_shard.argtypes = [vp, i, vp, i, u64, ctypes.c_uint, i, i, ctypes.POINTER(u64), pvp]
+    L.gm_g16_pk_save_cache.argtypes = [vp, vp, i]
+    L.gm_g16_pk_load_cache.argtypes = [vp, i, pvp]
+    L.gm_g16_stage_begin.argtypes = [vp, vp, sz, pvp]
+    L.gm_g16_stage_put_range.argtypes = [vp, i, sz, sz, vp]
+    L.gm_g16_stage_put_indexed.argtypes = [vp, i, vp, vp, sz]
+    L.gm_g16_stage_prove.argtypes = [vp, vp, vp, vp, vp, vp]
+    L.gm_g16_stage_free.argtypes = [vp]
     _lib = L
     return L
 
@@ -568,6 +581,70 @@ class ProvingKey:
         self.n, self.nb_wires, self.nb_public = domain_size, nb_wires, nb_public
         self.shard = (rank, world)
 
+    @classmethod
+    def from_dump(cls, ctx: Context, curve, path: str, offset: int, meta: dict, domain_size: int, nb_wires: int,
+                  nb_public: int, precompute: bool = False, shard=None):
+        """Streams the point slices of a gnark WriteDump file (marshal.go:389-456)
+        from byte `offset` into device buffers (gm_g16_pk_upload_dump_shard).
+        `meta` holds the header fields (g1_alpha, g1_beta, g1_delta, g2_beta,
+        g2_delta, infA, infB, optional k_wires) and the counts nbA / nbB / nbK.
+        Returns (key, end_offset)."""
+        self = cls.__new__(cls)
+        self.ctx = ctx
+        self.curve = curve_id(curve)
+        g1b, g2b = point_bytes(curve, False), point_bytes(curve, True)
+        stub = dict(meta)
+        for k, pb in (("g1_A", g1b), ("g1_B", g1b), ("g1_Z", g1b), ("g1_K", g1b), ("g2_B", g2b)):
+            stub[k] = np.zeros(pb, np.uint8)
+        counts = stub.pop("counts")
+        h, arrs = _pk_host_struct(curve, stub, domain_size, nb_wires, nb_public)
+        h.nbA, h.nbB = counts[0], counts[1]
+        if not ("k_wires" in meta and meta["k_wires"] is not None):
+            h.nbK = counts[2]
+        self._keep, self._h = arrs, h
+        handle, end = ctypes.c_void_p(), ctypes.c_uint64()
+        rank, world = shard if shard is not None else (0, 1)
+        fd = os.open(path, os.O_RDONLY)
+        try:
+            _check(load_library().gm_g16_pk_upload_dump_shard(ctx.handle, self.curve, ctypes.byref(h),
+                                                              fd, offset, self.PRECOMPUTE if precompute else 0,
+                                                              rank, world, ctypes.byref(end), ctypes.byref(handle)))
+        finally:
+            os.close(fd)
+        self.handle = handle
+        self.n, self.nb_wires, self.nb_public = domain_size, nb_wires, nb_public
+        self.shard = (rank, world)
+        return self, end.value
+
+    def save_cache(self, path: str):
+        """Device-layout copy of this key (gm_g16_pk_save_cache)."""
+        fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+        try:
+            _check(load_library().gm_g16_pk_save_cache(self.ctx.handle, self.handle, fd))
+        finally:
+            os.close(fd)
+
+    @classmethod
+    def from_cache(cls, ctx: Context, path: str, like: "ProvingKey" = None):
+        """Key read back from save_cache (gm_g16_pk_load_cache); `like` supplies
+        the host-side metadata (the host finishing only needs what the cache holds)."""
+        self = cls.__new__(cls)
+        self.ctx = ctx
+        handle = ctypes.c_void_p()
+        fd = os.open(path, os.O_RDONLY)
+        try:
+            _check(load_library().gm_g16_pk_load_cache(ctx.handle, fd, ctypes.byref(handle)))
+        finally:
+            os.close(fd)
+        self.handle = handle
+        if like is not None:
+            self.curve, self._h, self._keep = like.curve, like._h, like._keep
+            self.n, self.nb_wires, self.nb_public, self.shard = like.n, like.nb_wires, like.nb_public, like.shard
+        return self
+
+    def stage(self, nb_constraints: int) -> "Stage":
+        return Stage(self, nb_constraints)
+
     def free(self):
         if self.handle:
             load_library().gm_g16_pk_free(self.ctx.handle, self.handle)
@@ -600,6 +677,55 @@ class ProvingKey:
         _check(load_library().gm_g16_prove_partial(self.ctx.handle, self.handle, wires.ptr, a.ptr, b.ptr, c.ptr,
                                                    nb_constraints, _p(out)))
         return out.tobytes()
+
+
+class Stage:
+    """Prover inputs handed over while Solve runs (gm_g16_stage_*): put_range /
+    put_indexed per solver level (constraint/bn254/solver.go:426-532), then prove."""
+
+    A, B, C, WIRES = 0, 1, 2, 3
+
+    def __init__(self, pk: ProvingKey, nb_constraints: int):
+        self.pk = pk
+        h = ctypes.c_void_p()
+        _check(load_library().gm_g16_stage_begin(pk.ctx.handle, pk.handle, nb_constraints, ctypes.byref(h)))
+        self.handle = h
+
+    def put_range(self, which: int, lo: int, data):
+        d = _buf(data)
+        _check(load_library().gm_g16_stage_put_range(self.handle, which, lo, d.size // FR_BYTES, _p(d)))
+
+    def put_indexed(self, which: int, base, idx):
+        b = _buf(base)
+        ix = np.ascontiguousarray(np.asarray(idx, dtype=np.uint32))
+        _check(load_library().gm_g16_stage_put_indexed(self.handle, which, _p(b), ix.ctypes.data, ix.size))
+
+    def prove(self, r: bytes, s: bytes):
+        R, S = _buf(r), _buf(s)
+        ar = np.zeros(point_bytes(self.pk.curve, False), np.uint8)
+        krs = np.zeros(point_bytes(self.pk.curve, False), np.uint8)
+        bs = np.zeros(point_bytes(self.pk.curve, True), np.uint8)
+        _check(load_library().gm_g16_stage_prove(self.handle, _p(R), _p(S), _p(ar), _p(bs), _p(krs)))
+        return ar.tobytes(), bs.tobytes(), krs.tobytes()
+
+    def free(self):
+        if self.handle:
+            load_library().gm_g16_stage_free(self.handle)
+            self.handle = None
+
+
+def write_dump_slices(path: str, curve, pk: dict, prefix: bytes = b"") -> int:
+    """Writes `prefix` then pk's five point arrays as gnark-crypto
+    utils/unsafe.WriteSlice records in WriteDump order (marshal.go:430-444):
+    u64 little-endian count + raw points.  Returns the offset of the first
+    slice.  (Test / tooling helper: the real file comes from gnark's WriteDump.)"""
+    with open(path, "wb") as f:
+        f.write(prefix)
+        for key, g2 in (("g1_A", False), ("g1_B", False), ("g1_Z", False), ("g1_K", False), ("g2_B", True)):
+            raw = _buf(pk[key]).tobytes()
+            f.write(struct.pack("<Q", len(raw) // point_bytes(curve, g2)))
+            f.write(raw)
+    return len(prefix)
 
 
 class Multi:

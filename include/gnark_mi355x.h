@@ -273,6 +273,58 @@ int gm_g16_prove_multi(gm_multi* m, gm_g16_pk_multi* pk, const void* wires, cons
                        const void* c, size_t nb_constraints, const void* r, const void* s, void* ar_out,
                        void* bs_out, void* krs_out);
 
+/* ---- proving-key I/O --------------------------------
+ * gnark's ProvingKey.WriteDump (backend/groth16/bn254/marshal.go:389-456)
+ * writes, after its header (unsafe marker, Domain, the raw-encoded alpha /
+ * beta / delta, nbWires, NbInfinityA/B, InfinityA/B, nbCommitments), the five
+ * point slices G1.A, G1.B, G1.Z, G1.K, G2.B with gnark-crypto's
+ * utils/unsafe.WriteSlice: a little-endian uint64 element count followed by
+ * the raw G1Affine / G2Affine memory -- this ABI's point layout.
+ * gm_g16_pk_upload_dump reads those five slices from `fd` starting at byte
+ * `offset` (where ReadDump, marshal.go:511, starts reading them) and streams
+ * them into device buffers (pread into pinned buffers; H2D and conversion /
+ * GM_PK_PRECOMPUTE precomputation per 64 MiB chunk, overlapped with the
+ * reads).  `meta` carries the header fields as in gm_g16_pk_upload; its point
+ * pointers are ignored and its nbA / nbB / nbK (and domain_size - 1 for G1.Z)
+ * must equal the slice lengths in the file.  *end_offset receives the first
+ * byte after G2.B (the commitment keys' slices, marshal.go:532-543, follow).
+ * The _shard form reads only rank's slice of every array (as
+ * gm_g16_pk_upload_shard).  The file position of fd is not used or moved. */
+int gm_g16_pk_upload_dump(gm_ctx* ctx, int curve, const gm_g16_pk_host* meta, int fd, uint64_t offset,
+                          unsigned flags, uint64_t* end_offset, gm_g16_pk** out);
+int gm_g16_pk_upload_dump_shard(gm_ctx* ctx, int curve, const gm_g16_pk_host* meta, int fd, uint64_t offset,
+                                unsigned flags, int rank, int world, uint64_t* end_offset, gm_g16_pk** out);
+/* A device-resident key (shard) in its device layout, GM_PK_PRECOMPUTE window
+ * copies included, written to `fd` at its current position; load_cache reads
+ * one back with no conversion or precomputation (the persisted device form of
+ * SURVEY.md §5's checkpoint row). */
+int gm_g16_pk_save_cache(gm_ctx* ctx, const gm_g16_pk* pk, int fd);
+int gm_g16_pk_load_cache(gm_ctx* ctx, int fd, gm_g16_pk** out);
+
+/* ---- staged prover inputs --------------------------
+ * The R1CS solver (constraint/bn254/solver.go:426-532) makes a, b, c final
+ * level by level.  Each level (or range) can be handed over as soon as it is
+ * solved: every put copies its host data into a pinned ring before it returns
+ * (no host pointer is kept) and queues the copy to the device on the
+ * context's copy stream, so the H2D overlaps the rest of Solve.
+ * gm_g16_stage_prove waits for the queued copies and proves from the
+ * device-resident inputs (gm_g16_prove_device).  Every element of a, b, c
+ * [0, nb_constraints) and of the wires [0, nb_wires) must have been put; the
+ * prove consumes a, b, c (one proof per stage). */
+typedef struct gm_g16_stage gm_g16_stage;
+#define GM_STAGE_A 0
+#define GM_STAGE_B 1
+#define GM_STAGE_C 2
+#define GM_STAGE_WIRES 3
+int gm_g16_stage_begin(gm_ctx* ctx, gm_g16_pk* pk, size_t nb_constraints, gm_g16_stage** out);
+/* elements [lo, lo + count) of vector `which`; host_src points at element lo */
+int gm_g16_stage_put_range(gm_g16_stage* st, int which, size_t lo, size_t count, const void* host_src);
+/* elements idx[0..k) of vector `which` (one solver level), read from host_base[idx[j]] */
+int gm_g16_stage_put_indexed(gm_g16_stage* st, int which, const void* host_base, const uint32_t* idx, size_t k);
+int gm_g16_stage_prove(gm_g16_stage* st, const void* r, const void* s, void* ar_out, void* bs_out,
+                       void* krs_out);
+int gm_g16_stage_free(gm_g16_stage* st);
+
 /* ---- host-side group helpers (finishing adds of sharded MSMs) ---------- */
 /* out = p + q, all gnark Jacobian (G1Jac or G2Jac). */
 int gm_jac_add(int curve, int g2, const void* p, const void* q, void* out);
