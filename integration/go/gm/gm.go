@@ -192,6 +192,119 @@ func (k *G16Key) Prove(wires, a, b, c unsafe.Pointer, nbConstraints int, r, s, a
 	return nil
 }
 
+// UploadG16KeyDump streams the five point slices of a WriteDump file
+// (marshal.go:389-456) from f, starting at byte offset (where ReadDump,
+// marshal.go:511, starts reading them), straight into device buffers; k holds
+// the header fields (its point pointers are ignored).  Returns the offset just
+// past G2.B (the commitment keys' slices follow).  With several GPUs every
+// device streams its own shard of each array (gm_g16_pk_upload_dump_shard);
+// proofs then run per device and are summed on the host like UploadG16Key's.
+func UploadG16KeyDump(curve int, k *G16HostKey, f *os.File, offset int64, flags uint) (*G16Key, int64, error) {
+	ctx, err := Ctx()
+	if err != nil {
+		return nil, 0, err
+	}
+	if multi != nil {
+		return nil, 0, errors.New("gnark_mi355x: dump streaming drives one device; use UploadG16Key with several")
+	}
+	infA, infB := boolsToBytes(k.InfA), boolsToBytes(k.InfB)
+	h := C.gm_g16_pk_host{
+		domain_size: C.size_t(k.DomainSize), nb_wires: C.size_t(k.NbWires), nb_public: C.size_t(k.NbPublic),
+		nbA: C.size_t(k.NbA), nbB: C.size_t(k.NbB), nbK: C.size_t(k.NbK),
+		g1_alpha: k.Alpha, g1_beta: k.Beta, g1_delta: k.Delta,
+		g2_beta: k.Beta2, g2_delta: k.Delta2,
+		infA: (*C.uint8_t)(unsafe.Pointer(&infA[0])), infB: (*C.uint8_t)(unsafe.Pointer(&infB[0])),
+	}
+	if len(k.KWires) > 0 {
+		h.k_wires = (*C.uint32_t)(unsafe.Pointer(&k.KWires[0]))
+	}
+	key := &G16Key{curve: C.int(curve)}
+	var end C.uint64_t
+	if rc := C.gm_g16_pk_upload_dump(ctx, C.int(curve), &h, C.int(f.Fd()), C.uint64_t(offset), C.uint(flags), &end,
+		&key.single); rc != C.GM_OK {
+		return nil, 0, lastErr("gm_g16_pk_upload_dump", rc)
+	}
+	return key, int64(end), nil
+}
+
+// SaveCache writes the device copy of k (with its precomputed window copies)
+// to f in the device layout; LoadG16KeyCache reads it back with no conversion
+// or precomputation.
+func (k *G16Key) SaveCache(f *os.File) error {
+	if k.single == nil {
+		return errors.New("gnark_mi355x: SaveCache needs a single-device key")
+	}
+	if rc := C.gm_g16_pk_save_cache(ctx0, k.single, C.int(f.Fd())); rc != C.GM_OK {
+		return lastErr("gm_g16_pk_save_cache", rc)
+	}
+	return nil
+}
+
+func LoadG16KeyCache(curve int, f *os.File) (*G16Key, error) {
+	ctx, err := Ctx()
+	if err != nil {
+		return nil, err
+	}
+	key := &G16Key{curve: C.int(curve)}
+	if rc := C.gm_g16_pk_load_cache(ctx, C.int(f.Fd()), &key.single); rc != C.GM_OK {
+		return nil, lastErr("gm_g16_pk_load_cache", rc)
+	}
+	return key, nil
+}
+
+// Vectors of a staged proof (gm_g16_stage_*).
+const (
+	StageA     = C.GM_STAGE_A
+	StageB     = C.GM_STAGE_B
+	StageC     = C.GM_STAGE_C
+	StageWires = C.GM_STAGE_WIRES
+)
+
+// G16Stage collects a, b, c (and the wires) while the solver runs.
+type G16Stage struct{ h *C.gm_g16_stage }
+
+// Stage starts a staged proof of nbConstraints constraints (single device).
+func (k *G16Key) Stage(nbConstraints int) (*G16Stage, error) {
+	if k.single == nil {
+		return nil, errors.New("gnark_mi355x: staged inputs need a single-device key")
+	}
+	st := &G16Stage{}
+	if rc := C.gm_g16_stage_begin(ctx0, k.single, C.size_t(nbConstraints), &st.h); rc != C.GM_OK {
+		return nil, lastErr("gm_g16_stage_begin", rc)
+	}
+	return st, nil
+}
+
+// PutIndexed hands over base[idx[j]] of vector which (one solver level).
+func (st *G16Stage) PutIndexed(which int, base unsafe.Pointer, idx []uint32) error {
+	if len(idx) == 0 {
+		return nil
+	}
+	if rc := C.gm_g16_stage_put_indexed(st.h, C.int(which), base, (*C.uint32_t)(unsafe.Pointer(&idx[0])),
+		C.size_t(len(idx))); rc != C.GM_OK {
+		return lastErr("gm_g16_stage_put_indexed", rc)
+	}
+	return nil
+}
+
+// PutRange hands over elements [lo, lo+n) of vector which; src points at element lo.
+func (st *G16Stage) PutRange(which int, lo, n int, src unsafe.Pointer) error {
+	if rc := C.gm_g16_stage_put_range(st.h, C.int(which), C.size_t(lo), C.size_t(n), src); rc != C.GM_OK {
+		return lastErr("gm_g16_stage_put_range", rc)
+	}
+	return nil
+}
+
+// Prove waits for the staged copies and proves (Ar, Bs, Krs as G16Key.Prove).
+func (st *G16Stage) Prove(r, s, ar, bs, krs unsafe.Pointer) error {
+	if rc := C.gm_g16_stage_prove(st.h, r, s, ar, bs, krs); rc != C.GM_OK {
+		return lastErr("gm_g16_stage_prove", rc)
+	}
+	return nil
+}
+
+func (st *G16Stage) Free() { C.gm_g16_stage_free(st.h) }
+
 // ---------------------------------------------------------------------------
 // KZG (PLONK)
 // ---------------------------------------------------------------------------
