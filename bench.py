@@ -351,15 +351,17 @@ def groth16_bench(ctx, gm, logn, precompute=True, check_oracle=False):
         t0 = time.perf_counter()
         proof = dpk.prove(host[0], host[1], host[2], host[3], r[:32], r[32:])
         t_host.append(time.perf_counter() - t0)
-    dpk.free()
-    for b in [W, A, B, C] + srcs:
-        b.free()
     med = lambda v: sorted(v)[len(v) // 2]
     res = {"logn": logn, "pk": "precomputed" if precompute else "plain",
            "prove_ms_host_inputs": round(med(t_host) * 1e3, 3), "prove_ms_device_inputs": round(med(t_dev) * 1e3, 3),
            "runs": reps, "stat": "median",
            "scope": "host_inputs = icicle.go:204-412 incl. H2D of wires/a/b/c; device_inputs = same with inputs "
                     "resident; both after Solve"}
+    if check_oracle:
+        res.update(staged_and_io_bench(ctx, gm, dpk, pk, n, nb_wires, nb_public, host, r, proof))
+    dpk.free()
+    for b in [W, A, B, C] + srcs:
+        b.free()
     if check_oracle:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle_lib
@@ -369,6 +371,61 @@ def groth16_bench(ctx, gm, logn, precompute=True, check_oracle=False):
         res["oracle_s"] = round(time.perf_counter() - t0, 2)
         res["matches_oracle"] = bool(exp == proof)
     return res
+
+
+def staged_and_io_bench(ctx, gm, dpk, pk, n, nb_wires, nb_public, host, r, host_proof):
+    """SURVEY.md §8f rows 3-4 on the same key:
+      staged: a / b / c handed over in 64 "solver levels" and the wires in one
+              range before the timer starts (they overlap Solve), then the timed
+              gm_g16_stage_prove -- the prover latency left after Solve;
+      dump:   the key's five point arrays written as WriteDump slices
+              (marshal.go:389-456) to a local file, then streamed into device
+              buffers (gm_g16_pk_upload_dump) -- file read + H2D + conversion;
+      cache:  save / load of the device-layout key (gm_g16_pk_save_cache / load)."""
+    import tempfile
+    import numpy as np
+    out = {}
+    reps = 3
+    ts = []
+    for _ in range(reps):
+        st = dpk.stage(n)
+        for lo in range(0, n, n // 64):
+            for which, v in ((st.A, host[1]), (st.B, host[2]), (st.C, host[3])):
+                st.put_range(which, lo, v[32 * lo:32 * (lo + n // 64)])
+        st.put_range(st.WIRES, 0, host[0])
+        ctx.synchronize()
+        time.sleep(0.05)  # the copies finish during "Solve"
+        t0 = time.perf_counter()
+        proof = st.prove(r[:32], r[32:])
+        ts.append(time.perf_counter() - t0)
+        st.free()
+    out["prove_ms_staged_after_solve"] = round(sorted(ts)[reps // 2] * 1e3, 3)
+    out["staged_matches_host_scope"] = bool(proof == host_proof)
+    meta = {k: pk[k] for k in ("g1_alpha", "g1_beta", "g1_delta", "g2_beta", "g2_delta", "infA", "infB")}
+    meta["counts"] = (nb_wires, nb_wires, nb_wires - nb_public)
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "pk.dump")
+        off = gm.write_dump_slices(path, "bn254", pk, b"\0" * 4096)
+        nbytes = os.path.getsize(path) - off
+        t0 = time.perf_counter()
+        k2, _ = gm.ProvingKey.from_dump(ctx, "bn254", path, off, meta, n, nb_wires, nb_public)
+        t_dump = time.perf_counter() - t0
+        ok = k2.prove(host[0], host[1], host[2], host[3], r[:32], r[32:]) == proof
+        cpath = os.path.join(d, "pk.cache")
+        t0 = time.perf_counter()
+        k2.save_cache(cpath)
+        t_save = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        k3 = gm.ProvingKey.from_cache(ctx, cpath, like=k2)
+        t_load = time.perf_counter() - t0
+        ok = ok and k3.prove(host[0], host[1], host[2], host[3], r[:32], r[32:]) == proof
+        k2.free()
+        k3.free()
+    out["pk_dump"] = {"bytes": nbytes, "upload_s": round(t_dump, 4), "gb_per_s": round(nbytes / t_dump / 1e9, 2),
+                      "cache_save_s": round(t_save, 4), "cache_load_s": round(t_load, 4),
+                      "proofs_match": bool(ok),
+                      "note": "dump file in the page cache (local tmp); device-layout cache = same point bytes"}
+    return out
 
 
 def groth16_sharded_bench(ctx, gm, logn, rank, world, dist, torch):
@@ -446,6 +503,20 @@ def host_cpu():
         cores = len(os.sched_getaffinity(0))
     except AttributeError:
         cores = os.cpu_count() or 1
+    # the GPU box grants a CPU share through a cgroup quota while affinity and
+    # nproc show the whole machine: more threads than the quota only contend
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    if quota is None and os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        quota = int(os.environ["OMP_NUM_THREADS"])
+    if quota:
+        cores = min(cores, quota)
     model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:

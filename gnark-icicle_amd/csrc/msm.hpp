@@ -8,21 +8,24 @@ struct gm_ctx;
 
 namespace gm {
 struct Arena;
-// Two-level counting sort of the MSM digits (msm_impl.hpp pass 1, msm_sort.hip
-// pass 2).  T buckets; coarse bin H = bucket >> F (NC bins); M = upper bound on
-// the entries.  Coarse bins above S2_BIG entries are split into parts.
+// Counting sort of the MSM digits (msm_impl.hpp k_msm_digits, msm_sort.hip).
+// T buckets; coarse bin H = bucket >> F (NC bins, ~2K entries each for uniform
+// digits, finished in LDS); pass-1 bin = bucket >> (F + G) (NS bins).  G = 0:
+// two levels; G > 0: a middle pass splits each of the NS super-bins into its
+// 2^G coarse bins (large MSMs).  M = upper bound on the entries.  Coarse bins
+// above S2_BIG entries are split into parts.
 constexpr uint32_t S2_BIG = 1u << 16;
 constexpr uint32_t S2_STAGE = 6144;  // bins up to this many entries are sorted in LDS
 struct SortGeom {
-  uint32_t T = 0, F = 0, NC = 0;
+  uint32_t T = 0, F = 0, G = 0, NC = 0, NS = 0;
   size_t M = 0;
 };
-// Digits (k_msm_digits output, window-major, with the coarse counts) ->
-// sorted keys / values and offsets[0..T].  Scratch: cbase / pbase (NC + 1),
-// ccursor (NC), tmp (8 B x M), fcount (T).
-int msm_sort_digits(gm_ctx* ctx, const SortGeom& g, size_t n, uint32_t W, uint32_t nb, uint32_t shared_stride,
-                    const uint32_t* dig, const uint32_t* ccount, uint32_t* cbase, uint32_t* ccursor, uint32_t* pbase,
-                    uint64_t* tmp, uint32_t* fcount, uint32_t* keys_out, uint32_t* vals_out, uint32_t* offsets);
+// Digits (k_msm_digits output: window-major, plus the pass-1 bin counts
+// `scount`, NS words) -> sorted keys / values and offsets[0..T].  Scratch comes
+// from `arena`.
+int msm_sort_digits(gm_ctx* ctx, Arena& arena, const SortGeom& g, size_t n, uint32_t W, uint32_t nb,
+                    uint32_t shared_stride, const uint32_t* dig, const uint32_t* scount, uint32_t* keys_out,
+                    uint32_t* vals_out, uint32_t* offsets);
 
 // Fixed-base precomputation of a resident point set (a proving key's arrays):
 // W copies of the n points, copy w = [2^(c w)] P_i at index w * stride + i, so

@@ -59,7 +59,7 @@ GM_DEV FeG<Fr> load_scalar_canonical(const uint32_t* __restrict__ s, uint32_t i)
 // index | sign << 31.  Precomputed (shared-bucket) layout: b = |d|-1 for every
 // window, value = w*stride + i (the shifted copy) | sign << 31.
 struct DigitGeom {
-  uint32_t n, c, W, nb, shared_stride, F;  // F: fine bits of the sort (coarse bin = b >> F)
+  uint32_t n, c, W, nb, shared_stride, F;  // F: pass-1 bin = b >> F
 };
 
 // ---------------------------------------------------------------------------
@@ -389,6 +389,10 @@ __global__ void __launch_bounds__(128) k_msm_fixup_long(const uint32_t* __restri
 //   host: P_w = U + sum_b 2^(b + log2 L) Y_b, merged into the window Horner.
 // ---------------------------------------------------------------------------
 // node layout: per window, m nodes of Q = 2 + K XYZZ points [G, U, Y_0..Y_{K-1}]
+// At most 512 tree tasks (adds) per level: two per thread.  (A 512-thread
+// block with one task per thread measured no faster at 2^20: the tree's tail
+// is short of blocks, not of threads.)
+constexpr uint32_t BS_THREADS = 256;
 template <class F>
 __global__ void __launch_bounds__(128) k_msm_seg(const XYZZ<F>* __restrict__ buckets, uint32_t nb,
                                                  uint32_t L, uint32_t nseg, uint32_t W,
@@ -409,7 +413,7 @@ __global__ void __launch_bounds__(128) k_msm_seg(const XYZZ<F>* __restrict__ buc
 // One tree level group: block (w, j) merges nodes [j*NT, (j+1)*NT) of window w
 // (Qin points each) into one node of Qin + log2(NT) points.
 template <class F>
-__global__ void __launch_bounds__(256) k_msm_bitsum(const XYZZ<F>* __restrict__ in, uint32_t m,
+__global__ void __launch_bounds__(BS_THREADS) k_msm_bitsum(const XYZZ<F>* __restrict__ in, uint32_t m,
                                                     uint32_t Qin, uint32_t NT, uint32_t lgNT,
                                                     XYZZ<F>* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -521,28 +525,39 @@ int msm_plan(gm_ctx* ctx, Arena& arena, const void* scalars_dev, size_t n, const
     set_error("msm: n * windows must be < 2^31");
     return GM_ERR_INVALID;
   }
-  // Sort geometry: ~2K entries per coarse bin for uniform digits (pass 2 stages a
-  // bin of up to S2_STAGE entries in LDS; the narrow top window's bins are ~2x
-  // fuller), at most 8192 coarse bins and 2^13 fine bins per coarse bin.
+  // Sort geometry: ~2K entries per coarse bin for uniform digits (the final pass
+  // sorts a bin of up to S2_STAGE entries in LDS; the narrow top window's bins
+  // are ~2x fuller).  Pass-1 bins (b >> (F + G)) are coarsened by G until one
+  // pass-1 block (one window of S1 points in the plain layout) touches at most
+  // 512 of them (long write runs) and there are at most 8192; G > 0 adds the
+  // middle pass (msm_sort.hip).
   SortGeom sg;
   sg.T = plan.total;
   sg.M = M;
   sg.F = 4;
   while (sg.F < 13 && (double)M * std::ldexp(1.0, (int)sg.F + 1) <= 2048.0 * sg.T) sg.F++;
-  while (sg.F < 13 && ((sg.T + (1u << sg.F) - 1) >> sg.F) > 8192) sg.F++;
-  sg.NC = (sg.T + (1u << sg.F) - 1) >> sg.F;
-  if (sg.NC > 8192) {
+  auto bins = [&](uint32_t sh) { return (uint32_t)(((uint64_t)sg.T + (1ull << sh) - 1) >> sh); };
+  auto touched = [&](uint32_t sh) { return shared ? bins(sh) : std::max(1u, plan.nb >> sh); };
+  // GM_MSM_SORT_MING: minimum G (tests exercise the middle pass at small sizes)
+  const char* ming = getenv("GM_MSM_SORT_MING");
+  sg.G = ming ? (uint32_t)std::min(10, std::max(0, atoi(ming))) : 0u;
+  // (shared layout at 2^20: 8192 pass-1 bins with G = 0 measured 0.285 ms vs
+  // 0.315 with the middle pass, so only the plain layout uses the 512 rule)
+  const uint32_t max_touched = shared ? 8192u : 512u;
+  while (sg.G < 10 && (touched(sg.F + sg.G) > max_touched || bins(sg.F + sg.G) > 8192)) sg.G++;
+  while (sg.G && sg.F + sg.G > 31) sg.G--;
+  sg.NC = bins(sg.F);
+  sg.NS = bins(sg.F + sg.G);
+  if (sg.NS > 8192) {
     set_error("msm: too many buckets for the sort");
     return GM_ERR_INVALID;
   }
   int rc;
-  DevBuf dig, tmp, keys_out, vals_out, offsets, ccount, cbase, ccursor, pbase, fcount;
-  if ((rc = dig.alloc(arena, sizeof(uint32_t) * M)) || (rc = tmp.alloc(arena, sizeof(uint64_t) * M)) ||
-      (rc = keys_out.alloc(arena, sizeof(uint32_t) * M)) || (rc = vals_out.alloc(arena, sizeof(uint32_t) * M)) ||
+  DevBuf dig, keys_out, vals_out, offsets, scount;
+  if ((rc = dig.alloc(arena, sizeof(uint32_t) * M)) || (rc = keys_out.alloc(arena, sizeof(uint32_t) * M)) ||
+      (rc = vals_out.alloc(arena, sizeof(uint32_t) * M)) ||
       (rc = offsets.alloc(arena, sizeof(uint32_t) * ((size_t)plan.total + 1))) ||
-      (rc = ccount.alloc(arena, sizeof(uint32_t) * sg.NC)) || (rc = cbase.alloc(arena, sizeof(uint32_t) * (sg.NC + 1))) ||
-      (rc = ccursor.alloc(arena, sizeof(uint32_t) * sg.NC)) || (rc = pbase.alloc(arena, sizeof(uint32_t) * (sg.NC + 1))) ||
-      (rc = fcount.alloc(arena, sizeof(uint32_t) * (size_t)plan.total)))
+      (rc = scount.alloc(arena, sizeof(uint32_t) * sg.NS)))
     return rc;
   DigitGeom g;
   g.n = (uint32_t)n;
@@ -550,21 +565,20 @@ int msm_plan(gm_ctx* ctx, Arena& arena, const void* scalars_dev, size_t n, const
   g.W = W;
   g.nb = plan.nb;
   g.shared_stride = shared ? (uint32_t)pre->stride : 0u;
-  g.F = sg.F;
+  g.F = sg.F + sg.G;  // the digits kernel counts pass-1 bins
   {
     ProfScope ps(ctx, "msm_digits");
-    GM_HIP(hipMemsetAsync(ccount.p, 0, sizeof(uint32_t) * sg.NC, st));
+    GM_HIP(hipMemsetAsync(scount.p, 0, sizeof(uint32_t) * sg.NS, st));
     hipLaunchKernelGGL(k_msm_digits<typename C::Fr>, dim3(blocks_for(n, DG_THREADS * DG_PPT)), dim3(DG_THREADS),
-                       sizeof(uint32_t) * sg.NC, st, reinterpret_cast<const uint32_t*>(scalars_dev), g, sg.NC,
-                       dig.as<uint32_t>(), ccount.as<uint32_t>());
+                       sizeof(uint32_t) * sg.NS, st, reinterpret_cast<const uint32_t*>(scalars_dev), g, sg.NS,
+                       dig.as<uint32_t>(), scount.as<uint32_t>());
     GM_HIP(hipGetLastError());
   }
   {
     ProfScope ps(ctx, "msm_sort");
-    if ((rc = msm_sort_digits(ctx, sg, n, W, plan.nb, g.shared_stride, dig.as<uint32_t>(), ccount.as<uint32_t>(),
-                              cbase.as<uint32_t>(), ccursor.as<uint32_t>(), pbase.as<uint32_t>(),
-                              tmp.as<uint64_t>(), fcount.as<uint32_t>(), keys_out.as<uint32_t>(),
-                              vals_out.as<uint32_t>(), offsets.as<uint32_t>())))
+    if ((rc = msm_sort_digits(ctx, arena, sg, n, W, plan.nb, g.shared_stride, dig.as<uint32_t>(),
+                              scount.as<uint32_t>(), keys_out.as<uint32_t>(), vals_out.as<uint32_t>(),
+                              offsets.as<uint32_t>())))
       return rc;
   }
   plan.keys = keys_out.as<uint32_t>();
@@ -590,7 +604,13 @@ int msm_run(gm_ctx* ctx, const MsmPlan& plan, const void* points_internal,
   }
   const uint32_t c = plan.c, nb = plan.nb, total = plan.total, Wr = plan.Wred;
   const size_t M = plan.M;
-  const uint32_t L = nb >= 4 ? 4 : nb;  // level-1 segment length (buckets)
+  // level-1 segment length (buckets).  Measured at 2^20 (BN254 G1 / G2 /
+  // BLS12-377 G2 reduction ms): L = 1: 0.83 / 4.2 / 16.9, L = 2: 0.51 / 2.6 / 9.6,
+  // L = 4: 0.36 / 1.74 / 6.05 -- the LDS bit-sum trees cost more per add than the
+  // running sums.  GM_MSM_SEGL overrides (tuning).
+  static const int segl_env = getenv("GM_MSM_SEGL") ? atoi(getenv("GM_MSM_SEGL")) : 0;
+  const uint32_t Lwant = segl_env > 0 ? (uint32_t)segl_env : 4u;
+  const uint32_t L = nb >= Lwant ? Lwant : nb;
   const uint32_t nseg = nb / L;
   int rc;
 
@@ -645,14 +665,14 @@ int msm_run(gm_ctx* ctx, const MsmPlan& plan, const void* points_internal,
     while (m > 1) {
       uint32_t lg = 0;
       // largest power-of-two group with NT*Q slots in budget and <= 2 tasks per thread
-      while ((2u << lg) <= m && (size_t)(2u << lg) * Q <= SLOT_BUDGET && (1u << lg) * (Q + 1) <= 512) lg++;
+      while ((2u << lg) <= m && (size_t)(2u << lg) * Q <= SLOT_BUDGET && (1u << lg) * (Q + 1) <= 2 * BS_THREADS) lg++;
       if (lg == 0) {
         set_error("msm: bucket reduction does not fit LDS");
         return GM_ERR_INVALID;
       }
       const uint32_t NT = 1u << lg;
       const uint32_t groups = m / NT;
-      hipLaunchKernelGGL(k_msm_bitsum<DF>, dim3(Wr * groups), dim3(256), sizeof(XYZZ<DF>) * NT * Q, st, cur, m,
+      hipLaunchKernelGGL(k_msm_bitsum<DF>, dim3(Wr * groups), dim3(BS_THREADS), sizeof(XYZZ<DF>) * NT * Q, st, cur, m,
                          Q, NT, lg, nxt);
       Q += lg;
       m = groups;

@@ -27,7 +27,7 @@
 namespace gm {
 
 static __global__ void __launch_bounds__(1024) k_msm_s1_scan(const uint32_t* __restrict__ ccount, uint32_t NC,
-                                                             uint32_t T, uint32_t* __restrict__ cbase,
+                                                             uint32_t T, uint32_t psz, uint32_t* __restrict__ cbase,
                                                              uint32_t* __restrict__ ccursor,
                                                              uint32_t* __restrict__ pbase,
                                                              uint32_t* __restrict__ offsets) {
@@ -40,7 +40,7 @@ static __global__ void __launch_bounds__(1024) k_msm_s1_scan(const uint32_t* __r
     cbase[q] = a[q];
     ccursor[q] = a[q];
     const uint32_t cnt = ccount[q];
-    a[q] = cnt > S2_BIG ? (cnt + S2_BIG - 1) / S2_BIG : 1u;
+    a[q] = cnt > psz ? (cnt + psz - 1) / psz : 1u;
   }
   if (t == 0) {
     cbase[NC] = total;
@@ -107,6 +107,118 @@ __device__ __forceinline__ void s2_locate(const uint32_t* __restrict__ pbase, ui
     sh[1] = j - pbase[lo];
   }
   __syncthreads();
+}
+
+// ---- middle pass of a three-level sort (large MSMs) ------------------------
+// Pass 1 then partitions into super-bins s = b >> (F + G) (few enough that a
+// pass-1 block writes long runs), and this pass splits every super-bin into its
+// 2^G coarse bins H = b >> F, part by part (SM_PART entries): an LDS histogram
+// per part and global atomics give the coarse counts, a per-super-bin scan the
+// coarse bases (super-bin base + local prefix -- no device-wide scan), and the
+// scatter reserves one range per touched coarse bin (SM_PART / 2^G entries per
+// run on average).
+constexpr uint32_t SM_PART = 16384, SM_IPT = SM_PART / S_THREADS;
+
+static __global__ void __launch_bounds__(1024) k_msm_sm_count(const uint64_t* __restrict__ tmp,
+                                                              const uint32_t* __restrict__ sbase,
+                                                              const uint32_t* __restrict__ spbase, uint32_t NS,
+                                                              uint32_t F, uint32_t G, uint32_t* __restrict__ ccount) {
+  __shared__ uint32_t hist[1024], sh[2];
+  const uint32_t j = blockIdx.x, t = threadIdx.x;
+  if (j >= spbase[NS]) return;
+  s2_locate(spbase, NS, j, sh);
+  const uint32_t s = sh[0], p = sh[1];
+  const uint32_t start = sbase[s], cnt = sbase[s + 1] - start;
+  const uint32_t lo = p * SM_PART, hi = min(lo + SM_PART, cnt), ng = 1u << G;
+  for (uint32_t q = t; q < ng; q += S_THREADS) hist[q] = 0;
+  __syncthreads();
+  for (uint32_t e = lo + t; e < hi; e += S_THREADS) lds_rank_add(hist, ((uint32_t)tmp[start + e] >> F) & (ng - 1));
+  __syncthreads();
+  for (uint32_t q = t; q < ng; q += S_THREADS)
+    if (hist[q]) atomicAdd(&ccount[(s << G) + q], hist[q]);
+}
+
+// block s: coarse bases / cursors of super-bin s's 2^G coarse bins, and the
+// number of final-pass parts of each (cparts; > 1 only above S2_BIG entries)
+static __global__ void __launch_bounds__(1024) k_msm_sm_scan(const uint32_t* __restrict__ ccount,
+                                                             const uint32_t* __restrict__ sbase, uint32_t G,
+                                                             uint32_t NC, uint32_t* __restrict__ cbase,
+                                                             uint32_t* __restrict__ ccursor,
+                                                             uint32_t* __restrict__ cparts) {
+  __shared__ uint32_t a[1024], wsum[17];
+  const uint32_t s = blockIdx.x, t = threadIdx.x, H0 = s << G;
+  const uint32_t nh = min(1u << G, NC - H0);
+  for (uint32_t q = t; q < nh; q += S_THREADS) a[q] = ccount[H0 + q];
+  block_excl_scan(a, nh, wsum);
+  for (uint32_t q = t; q < nh; q += S_THREADS) {
+    const uint32_t c = ccount[H0 + q];
+    cbase[H0 + q] = sbase[s] + a[q];
+    ccursor[H0 + q] = sbase[s] + a[q];
+    cparts[H0 + q] = c > S2_BIG ? (c + S2_BIG - 1) / S2_BIG : 1u;
+  }
+  if (t == 0 && H0 + nh == NC) cbase[NC] = sbase[s + 1];
+}
+
+static __global__ void __launch_bounds__(1024) k_msm_sm_scatter(const uint64_t* __restrict__ tmp,
+                                                                const uint32_t* __restrict__ sbase,
+                                                                const uint32_t* __restrict__ spbase, uint32_t NS,
+                                                                uint32_t F, uint32_t G,
+                                                                uint32_t* __restrict__ ccursor,
+                                                                uint64_t* __restrict__ tmp2) {
+  __shared__ uint32_t hist[1024], cur[1024], sh[2];
+  const uint32_t j = blockIdx.x, t = threadIdx.x;
+  if (j >= spbase[NS]) return;
+  s2_locate(spbase, NS, j, sh);
+  const uint32_t s = sh[0], p = sh[1];
+  const uint32_t start = sbase[s], cnt = sbase[s + 1] - start;
+  const uint32_t lo = p * SM_PART, hi = min(lo + SM_PART, cnt), ng = 1u << G;
+  for (uint32_t q = t; q < ng; q += S_THREADS) hist[q] = 0;
+  __syncthreads();
+  uint64_t x[SM_IPT];
+  uint32_t rk[SM_IPT];
+#pragma unroll
+  for (uint32_t it = 0; it < SM_IPT; it++) {
+    const uint32_t e = lo + it * S_THREADS + t;
+    if (e < hi) {
+      x[it] = tmp[start + e];
+      rk[it] = lds_rank_add(hist, ((uint32_t)x[it] >> F) & (ng - 1));
+    }
+  }
+  __syncthreads();
+  for (uint32_t q = t; q < ng; q += S_THREADS)
+    if (hist[q]) cur[q] = atomicAdd(&ccursor[(s << G) + q], hist[q]);
+  __syncthreads();
+#pragma unroll
+  for (uint32_t it = 0; it < SM_IPT; it++) {
+    const uint32_t e = lo + it * S_THREADS + t;
+    if (e < hi) tmp2[cur[((uint32_t)x[it] >> F) & (ng - 1)] + rk[it]] = x[it];
+  }
+}
+
+// Device-wide exclusive scan of n u32 (out[n] = total): block scans of
+// SCAN_BLK elements, one block over the block totals, then the fix-up.
+constexpr uint32_t SCAN_BLK = 4096;
+static __global__ void __launch_bounds__(1024) k_scan_local(const uint32_t* __restrict__ in, uint32_t n,
+                                                            uint32_t* __restrict__ out, uint32_t* __restrict__ bsum) {
+  __shared__ uint32_t a[SCAN_BLK], wsum[17];
+  const uint32_t base = blockIdx.x * SCAN_BLK, len = min(SCAN_BLK, n - base);
+  for (uint32_t q = threadIdx.x; q < len; q += S_THREADS) a[q] = in[base + q];
+  const uint32_t tot = block_excl_scan(a, len, wsum);
+  for (uint32_t q = threadIdx.x; q < len; q += S_THREADS) out[base + q] = a[q];
+  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+static __global__ void __launch_bounds__(1024) k_scan_tops(uint32_t* __restrict__ bsum, uint32_t nblk) {
+  __shared__ uint32_t a[8192], wsum[17];
+  for (uint32_t q = threadIdx.x; q < nblk; q += S_THREADS) a[q] = bsum[q];
+  const uint32_t tot = block_excl_scan(a, nblk, wsum);
+  for (uint32_t q = threadIdx.x; q < nblk; q += S_THREADS) bsum[q] = a[q];
+  if (threadIdx.x == 0) bsum[nblk] = tot;
+}
+static __global__ void __launch_bounds__(1024) k_scan_add(uint32_t* __restrict__ out, uint32_t n,
+                                                          const uint32_t* __restrict__ bsum, uint32_t nblk) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] += bsum[i / SCAN_BLK];
+  if (i == 0) out[n] = bsum[nblk];
 }
 
 // LDS layout: hist[2^F] | staged keys[S2_STAGE] | staged values[S2_STAGE].
@@ -248,31 +360,73 @@ static __global__ void __launch_bounds__(1024) k_msm_s2_scatter(const uint64_t* 
   }
 }
 
-int msm_sort_digits(gm_ctx* ctx, const SortGeom& g, size_t n, uint32_t W, uint32_t nb, uint32_t shared_stride,
-                    const uint32_t* dig, const uint32_t* ccount, uint32_t* cbase, uint32_t* ccursor, uint32_t* pbase,
-                    uint64_t* tmp, uint32_t* fcount, uint32_t* keys_out, uint32_t* vals_out, uint32_t* offsets) {
-  if (g.NC == 0 || g.NC > 8192 || g.F > 13) {
+int msm_sort_digits(gm_ctx* ctx, Arena& arena, const SortGeom& g, size_t n, uint32_t W, uint32_t nb,
+                    uint32_t shared_stride, const uint32_t* dig, const uint32_t* scount, uint32_t* keys_out,
+                    uint32_t* vals_out, uint32_t* offsets) {
+  if (g.NS == 0 || g.NS > 8192 || g.F > 13 || g.G > 10 || g.NC != (g.T + (1u << g.F) - 1) >> g.F ||
+      g.NS != (g.T + (1u << (g.F + g.G)) - 1) >> (g.F + g.G)) {
     set_error("msm sort: bad geometry");
     return GM_ERR_INVALID;
   }
   hipStream_t st = ctx->stream;
-  hipLaunchKernelGGL(k_msm_s1_scan, dim3(1), dim3(S_THREADS), 0, st, ccount, g.NC, g.T, cbase, ccursor, pbase,
-                     offsets);
-  // coarse bins one window touches: its own nb >> F in the plain layout
-  const uint32_t nh = (!shared_stride && (1u << g.F) <= nb) ? nb >> g.F : g.NC;
+  const uint32_t shift = g.F + g.G;  // pass-1 bin = b >> shift (super-bin, or coarse bin when G = 0)
+  int rc;
+  DevBuf sbase, scursor, spbase, tmp;
+  if ((rc = sbase.alloc(arena, 4 * ((size_t)g.NS + 1))) || (rc = scursor.alloc(arena, 4 * (size_t)g.NS)) ||
+      (rc = spbase.alloc(arena, 4 * ((size_t)g.NS + 1))) || (rc = tmp.alloc(arena, 8 * g.M)))
+    return rc;
+  hipLaunchKernelGGL(k_msm_s1_scan, dim3(1), dim3(S_THREADS), 0, st, scount, g.NS, g.T, g.G ? SM_PART : S2_BIG,
+                     sbase.as<uint32_t>(), scursor.as<uint32_t>(), spbase.as<uint32_t>(), offsets);
+  // bins one pass-1 block touches: its window's own nb >> shift in the plain layout
+  const uint32_t nh = (!shared_stride && (1u << shift) <= nb) ? nb >> shift : g.NS;
   hipLaunchKernelGGL(k_msm_s1_scatter, dim3(blocks_for(n, S1_PTS), W), dim3(S_THREADS), 2 * sizeof(uint32_t) * nh, st,
-                     dig, (uint32_t)n, nb, shared_stride, g.F, g.NC, nh, ccursor, tmp);
+                     dig, (uint32_t)n, nb, shared_stride, shift, g.NS, nh, scursor.as<uint32_t>(), tmp.as<uint64_t>());
+  // final pass input: coarse-binned entries with their bases / part table
+  const uint64_t* fin = tmp.as<uint64_t>();
+  const uint32_t *cbase = sbase.as<uint32_t>(), *pbase = spbase.as<uint32_t>();
+  if (g.G) {
+    DevBuf ccount, cb, ccur, cparts, pb, bsum, tmp2;
+    const uint32_t nblk = (g.NC + SCAN_BLK - 1) / SCAN_BLK;
+    if ((rc = ccount.alloc(arena, 4 * (size_t)g.NC)) || (rc = cb.alloc(arena, 4 * ((size_t)g.NC + 1))) ||
+        (rc = ccur.alloc(arena, 4 * (size_t)g.NC)) || (rc = cparts.alloc(arena, 4 * (size_t)g.NC)) ||
+        (rc = pb.alloc(arena, 4 * ((size_t)g.NC + 1))) || (rc = bsum.alloc(arena, 4 * ((size_t)nblk + 1))) ||
+        (rc = tmp2.alloc(arena, 8 * g.M)))
+      return rc;
+    if (nblk > 8192) {
+      set_error("msm sort: too many coarse bins");
+      return GM_ERR_INVALID;
+    }
+    const size_t mparts = (size_t)g.NS + g.M / SM_PART + 1;
+    GM_HIP(hipMemsetAsync(ccount.p, 0, 4 * (size_t)g.NC, st));
+    hipLaunchKernelGGL(k_msm_sm_count, dim3((unsigned)mparts), dim3(S_THREADS), 0, st, tmp.as<uint64_t>(),
+                       sbase.as<uint32_t>(), spbase.as<uint32_t>(), g.NS, g.F, g.G, ccount.as<uint32_t>());
+    hipLaunchKernelGGL(k_msm_sm_scan, dim3(g.NS), dim3(S_THREADS), 0, st, ccount.as<uint32_t>(), sbase.as<uint32_t>(),
+                       g.G, g.NC, cb.as<uint32_t>(), ccur.as<uint32_t>(), cparts.as<uint32_t>());
+    hipLaunchKernelGGL(k_scan_local, dim3(nblk), dim3(S_THREADS), 0, st, cparts.as<uint32_t>(), g.NC,
+                       pb.as<uint32_t>(), bsum.as<uint32_t>());
+    hipLaunchKernelGGL(k_scan_tops, dim3(1), dim3(S_THREADS), 0, st, bsum.as<uint32_t>(), nblk);
+    hipLaunchKernelGGL(k_scan_add, dim3(blocks_for(g.NC, 256)), dim3(256), 0, st, pb.as<uint32_t>(), g.NC,
+                       bsum.as<uint32_t>(), nblk);
+    hipLaunchKernelGGL(k_msm_sm_scatter, dim3((unsigned)mparts), dim3(S_THREADS), 0, st, tmp.as<uint64_t>(),
+                       sbase.as<uint32_t>(), spbase.as<uint32_t>(), g.NS, g.F, g.G, ccur.as<uint32_t>(),
+                       tmp2.as<uint64_t>());
+    fin = tmp2.as<uint64_t>();
+    cbase = cb.as<uint32_t>();
+    pbase = pb.as<uint32_t>();
+  }
+  DevBuf fcount;
+  if ((rc = fcount.alloc(arena, 4 * (size_t)g.T))) return rc;
   const uint32_t nfmax = std::min<uint32_t>(1u << g.F, g.T);
   // every coarse bin has >= 1 part; split bins add at most M / S2_BIG more
   const size_t maxparts = (size_t)g.NC + g.M / S2_BIG + 1;
-  GM_HIP(hipMemsetAsync(fcount, 0, sizeof(uint32_t) * g.T, st));
+  GM_HIP(hipMemsetAsync(fcount.p, 0, sizeof(uint32_t) * g.T, st));
   hipLaunchKernelGGL(k_msm_s2_local, dim3((unsigned)maxparts), dim3(S_THREADS),
-                     sizeof(uint32_t) * (nfmax + 2 * S2_STAGE), st, tmp, cbase, pbase, g.NC, g.F, g.T, fcount,
-                     keys_out, vals_out, offsets);
+                     sizeof(uint32_t) * (nfmax + 2 * S2_STAGE), st, fin, cbase, pbase, g.NC, g.F, g.T,
+                     fcount.as<uint32_t>(), keys_out, vals_out, offsets);
   hipLaunchKernelGGL(k_msm_s2_scan, dim3(g.NC), dim3(S_THREADS), sizeof(uint32_t) * nfmax, st, cbase, g.F, g.T,
-                     fcount, offsets);
+                     fcount.as<uint32_t>(), offsets);
   hipLaunchKernelGGL(k_msm_s2_scatter, dim3((unsigned)maxparts), dim3(S_THREADS), 2 * sizeof(uint32_t) * nfmax, st,
-                     tmp, cbase, pbase, g.NC, g.F, g.T, fcount, keys_out, vals_out);
+                     fin, cbase, pbase, g.NC, g.F, g.T, fcount.as<uint32_t>(), keys_out, vals_out);
   GM_HIP(hipGetLastError());
   return GM_OK;
 }

@@ -29,7 +29,8 @@ import struct
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libgnark_mi355x.so")
+# GNARK_MI355X_LIB: an alternative build of the same library (same-box A/B runs)
+LIB_PATH = os.environ.get("GNARK_MI355X_LIB") or os.path.join(HERE, "libgnark_mi355x.so")
 
 BN254, BLS12_377 = 0, 1
 CURVES = {"bn254": BN254, "bls12377": BLS12_377}

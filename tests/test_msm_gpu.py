@@ -358,3 +358,48 @@ def test_msm_split_coarse_bin(gm_ctx, oracle, value):
     finally:
         for b in (S, K, P):
             b.free()
+
+
+@pytest.mark.parametrize("cname,g2,window,pre", [("bn254", False, 16, False), ("bn254", False, 0, True),
+                                                 ("bls12377", True, 0, False), ("bn254", True, 0, True)])
+def test_msm_three_level_sort_vs_oracle(gm_ctx, oracle, monkeypatch, cname, g2, window, pre):
+    """The middle pass of the bucket sort (pass-1 super-bins split into coarse
+    bins, msm_sort.hip) runs by itself only for large MSMs (2^22+, precomputed
+    2^20+); GM_MSM_SORT_MING forces it here, at several depths."""
+    import gnark_mi355x as gm
+    n = (1 << 14) + 11
+    S = gm_ctx.random_scalars(cname, n, seed=0x3EED0007)
+    K = gm_ctx.random_scalars(cname, n, seed=0x3EED1007)
+    P = gm_ctx.batch_mul_base(cname, g2, gm.generator(cname, g2), K, n)
+    exp = oracle.msm(cname, g2, S.to_host(), P.to_host())
+    pts = gm_ctx.points_upload_precomputed(cname, P.to_host(), g2, window) if pre else None
+    try:
+        for ming in (1, 3, 6):
+            monkeypatch.setenv("GM_MSM_SORT_MING", str(ming))
+            gm_ctx.set_msm_window(0 if pre else window)
+            if pre:
+                got = gm_ctx.msm_precomputed(cname, S, pts, n, g2)[1]
+            else:
+                got = gm_ctx.msm(cname, S, P, n, g2)[1]
+            assert got == exp, ming
+    finally:
+        gm_ctx.set_msm_window(0)
+        for b in (S, K, P) + ((pts,) if pre else ()):
+            b.free()
+
+
+def test_msm_three_level_sort_skewed(gm_ctx, oracle, monkeypatch):
+    """Middle pass + split final bins: one bucket of 2^19 + 5 entries."""
+    import gnark_mi355x as gm
+    monkeypatch.setenv("GM_MSM_SORT_MING", "2")
+    c = pyref.CURVES["bn254"]
+    n = (1 << 19) + 5
+    sb = pyref.encode_fr(c, 2) * n
+    K = gm_ctx.random_scalars("bn254", n, seed=0x5118)
+    P = gm_ctx.batch_mul_base("bn254", False, gm.generator("bn254", False), K, n)
+    S = gm_ctx.copy_to_device(sb)
+    try:
+        assert gm_ctx.msm("bn254", S, P, n, False)[1] == oracle.msm("bn254", False, sb, P.to_host())
+    finally:
+        for b in (S, K, P):
+            b.free()
