@@ -156,8 +156,12 @@ int gm_destroy(gm_ctx* ctx) {
   if (ctx->aux) hipStreamSynchronize(ctx->aux);
   if (ctx->copy) hipStreamSynchronize(ctx->copy);
   ntt_domains_free(ctx);
-  for (auto& ch : ctx->chunks) hipFree(ch.base);
-  ctx->chunks.clear();
+  for (gm::ArenaState* a : {&ctx->arena, &ctx->slots[0], &ctx->slots[1]}) {
+    for (auto& ch : a->chunks) hipFree(ch.base);
+    a->chunks.clear();
+  }
+  for (void* p : ctx->tail_pinned)
+    if (p) hipHostFree(p);
   for (auto e : ctx->event_pool) hipEventDestroy(e);
   for (auto& p : ctx->pending) {
     hipEventDestroy(p.a);
@@ -290,6 +294,77 @@ int gm_msm(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const void* 
     rc = g2 ? msm_to_host<CurveBLS12377, true>(ctx, scalars_dev, points_dev, n, out_jac, out_affine)
             : msm_to_host<CurveBLS12377, false>(ctx, scalars_dev, points_dev, n, out_jac, out_affine);
   prof_collect(ctx);
+  return rc;
+}
+
+}  // extern "C"
+
+struct gm_msm_pending {
+  gm_ctx* ctx;
+  int curve, g2;
+  gm::SlotArena slot;
+  gm::MsmTail tail;
+  explicit gm_msm_pending(gm_ctx* c) : ctx(c), slot(c) {}
+};
+
+namespace {
+template <class C, bool G2>
+int msm_wait_t(gm_msm_pending* p, void* out_jac, void* out_aff) {
+  using HF = typename GroupSel<C, G2>::HF;
+  HF j[3];
+  int rc = msm_finish<C, G2>(p->ctx, p->tail, j);
+  if (rc) return rc;
+  if (out_jac) memcpy(out_jac, j, sizeof(j));
+  if (out_aff) {
+    host::Aff<HF> a = host::to_aff(host::Jac<HF>{j[0], j[1], j[2]});
+    memcpy(out_aff, &a, sizeof(a));
+  }
+  return GM_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int gm_msm_async(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const void* points_dev, size_t n,
+                 gm_msm_pending** out) {
+  if (!ctx || !out) return GM_ERR_INVALID;
+  if (int rc = check_curve(curve)) return rc;
+  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  GM_HIP(hipSetDevice(ctx->device));
+  auto* p = new gm_msm_pending(ctx);
+  p->curve = curve;
+  p->g2 = g2 ? 1 : 0;
+  int rc = p->slot.take();
+  if (rc == GM_OK) {
+    Arena& a = *p->slot.a;
+    if (curve == GM_BN254)
+      rc = g2 ? msm_device_launch<CurveBN254, true>(ctx, a, scalars_dev, points_dev, n, false, nullptr, p->tail)
+              : msm_device_launch<CurveBN254, false>(ctx, a, scalars_dev, points_dev, n, false, nullptr, p->tail);
+    else
+      rc = g2 ? msm_device_launch<CurveBLS12377, true>(ctx, a, scalars_dev, points_dev, n, false, nullptr, p->tail)
+              : msm_device_launch<CurveBLS12377, false>(ctx, a, scalars_dev, points_dev, n, false, nullptr, p->tail);
+  }
+  if (rc) {
+    delete p;
+    return rc;
+  }
+  *out = p;
+  return GM_OK;
+}
+
+int gm_msm_wait(gm_msm_pending* p, void* out_jac, void* out_affine) {
+  if (!p) return GM_ERR_INVALID;
+  gm_ctx* ctx = p->ctx;
+  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  GM_HIP(hipSetDevice(ctx->device));
+  int rc;
+  if (p->curve == GM_BN254)
+    rc = p->g2 ? msm_wait_t<CurveBN254, true>(p, out_jac, out_affine) : msm_wait_t<CurveBN254, false>(p, out_jac, out_affine);
+  else
+    rc = p->g2 ? msm_wait_t<CurveBLS12377, true>(p, out_jac, out_affine)
+               : msm_wait_t<CurveBLS12377, false>(p, out_jac, out_affine);
+  prof_collect(ctx);
+  delete p;
   return rc;
 }
 

@@ -431,24 +431,34 @@ int g16_sums_t(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, HSource& hs, G
   const MsmPrecomp* pB = pk->precomp ? &pk->preB : nullptr;
   const MsmPrecomp* pK = pk->precomp ? &pk->preK : nullptr;
   const MsmPrecomp* pZ = pk->precomp ? &pk->preZ : nullptr;
-  if ((rc = hs.poll())) return rc;
-  if ((rc = msm_device<C, false>(ctx, wA.p, pk->A, pk->nbA, out.A, true, pA))) return rc;
-  if ((rc = hs.poll())) return rc;
-  {
-    // the G1 and G2 B-MSMs (prove.go:217,293) share scalars and layout: one plan
-    Arena parena(ctx);
-    MsmPlan planB;
-    if ((rc = msm_plan<C>(ctx, parena, wB.p, pk->nbB, pB, planB))) return rc;
-    if ((rc = msm_run<C, false>(ctx, planB, pk->B, out.B))) return rc;
-    if (on_ab) on_ab(out);
-    if ((rc = hs.poll())) return rc;
-    if ((rc = msm_run<C, true>(ctx, planB, pk->B2, out.B2))) return rc;
-  }
-  if ((rc = hs.poll())) return rc;
-  if ((rc = msm_device<C, false>(ctx, wK.p, pk->K, pk->nbK, out.K, true, pK))) return rc;
+  // The five MSMs run pipelined two deep: the host tail of one (readback checks
+  // and Horner, msm_finish) overlaps the device work of the next, each MSM in
+  // one of the context's two slot arenas.  The G1 and G2 B-MSMs
+  // (prove.go:217,293) share scalars and layout: one plan, in slot 1.
+  SlotArena s0(ctx), s1(ctx);
+  MsmTail tA, tB, tB2, tK, tZ;
+  if ((rc = hs.poll()) || (rc = s0.take())) return rc;
+  if ((rc = msm_device_launch<C, false>(ctx, *s0.a, wA.p, pk->A, pk->nbA, true, pA, tA))) return rc;
+  if ((rc = hs.poll()) || (rc = s1.take())) return rc;
+  MsmPlan planB;
+  if ((rc = msm_plan<C>(ctx, *s1.a, wB.p, pk->nbB, pB, planB)) ||
+      (rc = msm_launch<C, false>(ctx, *s1.a, planB, pk->B, tB)))
+    return rc;
+  if ((rc = msm_finish<C, false>(ctx, tA, out.A))) return rc;
+  s0.release();
+  if ((rc = hs.poll()) || (rc = msm_launch<C, true>(ctx, *s1.a, planB, pk->B2, tB2))) return rc;
+  if ((rc = msm_finish<C, false>(ctx, tB, out.B))) return rc;
+  if (on_ab) on_ab(out);
+  if ((rc = hs.poll()) || (rc = s0.take())) return rc;
+  if ((rc = msm_device_launch<C, false>(ctx, *s0.a, wK.p, pk->K, pk->nbK, true, pK, tK))) return rc;
+  if ((rc = msm_finish<C, true>(ctx, tB2, out.B2))) return rc;
+  s1.release();
   const void* zs = nullptr;
-  if ((rc = hs.z_scalars(&zs))) return rc;
-  return msm_device<C, false>(ctx, zs, pk->Z, pk->nbZ, out.Z, true, pZ);
+  if ((rc = hs.z_scalars(&zs)) || (rc = s1.take())) return rc;
+  if ((rc = msm_device_launch<C, false>(ctx, *s1.a, zs, pk->Z, pk->nbZ, true, pZ, tZ))) return rc;
+  if ((rc = msm_finish<C, false>(ctx, tK, out.K))) return rc;
+  s0.release();
+  return msm_finish<C, false>(ctx, tZ, out.Z);
 }
 
 // Host finishing of icicle.go:280-391 / prove.go:183-305 from the raw sums:

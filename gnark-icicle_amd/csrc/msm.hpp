@@ -2,6 +2,7 @@
 #pragma once
 #include <cstddef>
 #include <cstdint>
+#include <hip/hip_runtime.h>
 #include "curves.hpp"
 
 struct gm_ctx;
@@ -60,6 +61,32 @@ int msm_plan(gm_ctx* ctx, Arena& arena, const void* scalars_dev, size_t n, const
 template <class C, bool G2>
 int msm_run(gm_ctx* ctx, const MsmPlan& plan, const void* points_internal,
             typename GroupSel<C, G2>::HF (&jac_out)[3]);
+
+// An MSM whose device work is queued and whose host tail (consistency and
+// long-span checks, host Horner) is deferred to msm_finish, so that the tail of
+// one MSM overlaps the device work of the next.  Its buffers live in the Arena
+// given to msm_launch, which must outlive msm_finish.
+struct MsmTail {
+  size_t n = 0, M = 0;
+  uint32_t c = 0, W = 0, Wr = 0, nb = 0, total = 0, L = 0, nseg = 0, K = 0, Q = 2;
+  const uint32_t* keys = nullptr;
+  const uint32_t* offsets = nullptr;
+  void *buckets = nullptr, *pfirst = nullptr, *plast = nullptr, *nodes_a = nullptr, *nodes_b = nullptr;
+  void *wsum = nullptr, *errw = nullptr;
+  uint8_t* stage = nullptr;  // pinned readback: 16 B (error, max span) + the exported nodes
+  hipEvent_t done = nullptr;
+  ~MsmTail() {
+    if (done) hipEventDestroy(done);
+  }
+};
+template <class C, bool G2>
+int msm_launch(gm_ctx* ctx, Arena& arena, const MsmPlan& plan, const void* points_internal, MsmTail& t);
+template <class C, bool G2>
+int msm_finish(gm_ctx* ctx, MsmTail& t, typename GroupSel<C, G2>::HF (&jac_out)[3]);
+// plan + launch (points converted into `arena` first unless points_internal)
+template <class C, bool G2>
+int msm_device_launch(gm_ctx* ctx, Arena& arena, const void* scalars_dev, const void* points_dev, size_t n,
+                      bool points_internal, const MsmPrecomp* pre, MsmTail& t);
 
 // out = sum_i int(scalars[i]) * points[i] as a host Jacobian triple (X, Y, Z).
 // points_dev is gnark-layout affine points, or (points_internal) an array of

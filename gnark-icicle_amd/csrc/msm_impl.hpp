@@ -587,51 +587,121 @@ int msm_plan(gm_ctx* ctx, Arena& arena, const void* scalars_dev, size_t n, const
   return GM_OK;
 }
 
-// Bucket accumulation, reduction and the host Horner tail over a plan.
+// Bucket reduction of a launched MSM (k_msm_seg, LDS bit-sum levels, export
+// into t.wsum); sets t.Q, the points per exported node.
 template <class C, bool G2>
-int msm_run(gm_ctx* ctx, const MsmPlan& plan, const void* points_internal,
-            typename GroupSel<C, G2>::HF (&jac_out)[3]) {
+int msm_reduce(gm_ctx* ctx, MsmTail& t) {
+  using DF = typename GroupSel<C, G2>::DF;
+  hipStream_t st = ctx->stream;
+  ProfScope ps(ctx, "msm_bucket_reduce");
+  uint32_t Q = 2;  // points per node: [G, U, Y_0..Y_{Q-3}]
+  hipLaunchKernelGGL(k_msm_seg<DF>, dim3(blocks_for((size_t)t.Wr * t.nseg, 128)), dim3(128), 0, st,
+                     (const XYZZ<DF>*)t.buckets, t.nb, t.L, t.nseg, t.Wr, (XYZZ<DF>*)t.nodes_a);
+  // LDS tree levels until one node per window
+  constexpr size_t SLOT_BUDGET = (96u << 10) / sizeof(XYZZ<DF>);
+  uint32_t m = t.nseg;
+  XYZZ<DF>* cur = (XYZZ<DF>*)t.nodes_a;
+  XYZZ<DF>* nxt = (XYZZ<DF>*)t.nodes_b;
+  while (m > 1) {
+    uint32_t lg = 0;
+    // largest power-of-two group with NT*Q slots in budget and <= 2 tasks per thread
+    while ((2u << lg) <= m && (size_t)(2u << lg) * Q <= SLOT_BUDGET && (1u << lg) * (Q + 1) <= 2 * BS_THREADS) lg++;
+    if (lg == 0) {
+      set_error("msm: bucket reduction does not fit LDS");
+      return GM_ERR_INVALID;
+    }
+    const uint32_t NT = 1u << lg;
+    const uint32_t groups = m / NT;
+    hipLaunchKernelGGL(k_msm_bitsum<DF>, dim3(t.Wr * groups), dim3(BS_THREADS), sizeof(XYZZ<DF>) * NT * Q, st, cur,
+                       m, Q, NT, lg, nxt);
+    Q += lg;
+    m = groups;
+    std::swap(cur, nxt);
+  }
+  hipLaunchKernelGGL(k_msm_export<DF>, dim3(blocks_for((size_t)t.Wr * Q, 128)), dim3(128), 0, st, cur, t.Wr * Q,
+                     (uint32_t*)t.wsum);
+  GM_HIP(hipGetLastError());
+  t.Q = Q;
+  return GM_OK;
+}
+
+// Buckets spanning more than FIX_SERIAL slices: tree fixup over part_first.
+template <class C, bool G2>
+int msm_fix_long(gm_ctx* ctx, MsmTail& t, uint32_t maxspan) {
+  using DF = typename GroupSel<C, G2>::DF;
+  hipStream_t st = ctx->stream;
+  const size_t nslices = (t.M + t.K - 1) / t.K;
+  for (uint32_t d = 0; (1u << d) < maxspan; d++)
+    hipLaunchKernelGGL(k_msm_fix_tree<DF>, dim3(blocks_for(nslices, 128)), dim3(128), 0, st, t.keys, t.offsets,
+                       t.total, t.K, (uint32_t)nslices, d, (XYZZ<DF>*)t.pfirst);
+  hipLaunchKernelGGL(k_msm_fixup_long<DF>, dim3(blocks_for(t.total, 128)), dim3(128), 0, st, t.offsets, t.total,
+                     t.K, (XYZZ<DF>*)t.buckets, (const XYZZ<DF>*)t.pfirst, (const XYZZ<DF>*)t.plast);
+  GM_HIP(hipGetLastError());
+  return GM_OK;
+}
+
+// readback of (error, max span) and the exported nodes into t.stage, event after it
+template <class C, bool G2>
+int msm_readback(gm_ctx* ctx, MsmTail& t) {
+  using DF = typename GroupSel<C, G2>::DF;
+  constexpr int WORDS = Coord<DF>::WORDS;
+  hipStream_t st = ctx->stream;
+  const size_t wbytes = sizeof(uint32_t) * 4 * WORDS * t.Wr * t.Q;
+  if (int r = tail_pinned_buf(ctx, 16 + wbytes, &t.stage)) return r;
+  GM_HIP(hipMemcpyAsync(t.stage, t.errw, 16, hipMemcpyDeviceToHost, st));
+  GM_HIP(hipMemcpyAsync(t.stage + 16, t.wsum, wbytes, hipMemcpyDeviceToHost, st));
+  if (!t.done) GM_HIP(hipEventCreateWithFlags(&t.done, hipEventDisableTiming));
+  GM_HIP(hipEventRecord(t.done, st));
+  return GM_OK;
+}
+
+// Bucket accumulation and (speculative) reduction over a plan, queued on the
+// context's stream; msm_finish completes it.
+template <class C, bool G2>
+int msm_launch(gm_ctx* ctx, Arena& arena, const MsmPlan& plan, const void* points_internal, MsmTail& t) {
   using DF = typename GroupSel<C, G2>::DF;
   using HF = typename GroupSel<C, G2>::HF;
-  using HJ = host::Jac<HF>;
   hipStream_t st = ctx->stream;
-  if (plan.n == 0) {
-    HJ inf = HJ::inf();
-    jac_out[0] = inf.x;
-    jac_out[1] = inf.y;
-    jac_out[2] = inf.z;
-    return GM_OK;
-  }
-  const uint32_t c = plan.c, nb = plan.nb, total = plan.total, Wr = plan.Wred;
-  const size_t M = plan.M;
+  t.n = plan.n;
+  if (plan.n == 0) return GM_OK;
+  t.c = plan.c;
+  t.W = plan.W;
+  t.nb = plan.nb;
+  t.total = plan.total;
+  t.Wr = plan.Wred;
+  t.M = plan.M;
+  t.keys = plan.keys;
+  t.offsets = plan.offsets;
   // level-1 segment length (buckets).  Measured at 2^20 (BN254 G1 / G2 /
   // BLS12-377 G2 reduction ms): L = 1: 0.83 / 4.2 / 16.9, L = 2: 0.51 / 2.6 / 9.6,
   // L = 4: 0.36 / 1.74 / 6.05 -- the LDS bit-sum trees cost more per add than the
   // running sums.  GM_MSM_SEGL overrides (tuning).
   static const int segl_env = getenv("GM_MSM_SEGL") ? atoi(getenv("GM_MSM_SEGL")) : 0;
   const uint32_t Lwant = segl_env > 0 ? (uint32_t)segl_env : 4u;
-  const uint32_t L = nb >= Lwant ? Lwant : nb;
-  const uint32_t nseg = nb / L;
+  t.L = t.nb >= Lwant ? Lwant : t.nb;
+  t.nseg = t.nb / t.L;
+  t.K = ctx->msm_slice ? (uint32_t)ctx->msm_slice : 64u;
   int rc;
-
-  Arena arena(ctx);
   constexpr int WORDS = Coord<DF>::WORDS;  // u32 words of one gnark-layout coordinate
-  DevBuf buckets, nodes_a, nodes_b, wsum, errw;
-  if ((rc = errw.alloc(arena, 16))) return rc;
+  static_assert(sizeof(HF) == 4 * WORDS, "host/device layout mismatch");
+  const size_t nslices = (t.M + t.K - 1) / t.K;
+  DevBuf buckets, nodes_a, nodes_b, wsum, errw, pfirst, plast;
+  if ((rc = errw.alloc(arena, 16)) || (rc = buckets.alloc(arena, sizeof(XYZZ<DF>) * (size_t)t.total)) ||
+      (rc = nodes_a.alloc(arena, sizeof(XYZZ<DF>) * 2 * (size_t)t.Wr * t.nseg)) ||
+      (rc = nodes_b.alloc(arena, sizeof(XYZZ<DF>) * 2 * (size_t)t.Wr * t.nseg)) ||
+      (rc = wsum.alloc(arena, sizeof(uint32_t) * 4 * WORDS * t.Wr * (2 + t.c))) ||
+      (rc = pfirst.alloc(arena, sizeof(XYZZ<DF>) * nslices)) || (rc = plast.alloc(arena, sizeof(XYZZ<DF>) * nslices)))
+    return rc;
+  t.buckets = buckets.p;
+  t.nodes_a = nodes_a.p;
+  t.nodes_b = nodes_b.p;
+  t.wsum = wsum.p;
+  t.errw = errw.p;
+  t.pfirst = pfirst.p;
+  t.plast = plast.p;
   GM_HIP(hipMemsetAsync(errw.p, 0, 16, st));
-  if ((rc = buckets.alloc(arena, sizeof(XYZZ<DF>) * (size_t)total))) return rc;
-  if ((rc = nodes_a.alloc(arena, sizeof(XYZZ<DF>) * 2 * (size_t)Wr * nseg))) return rc;
-  if ((rc = nodes_b.alloc(arena, sizeof(XYZZ<DF>) * 2 * (size_t)Wr * nseg))) return rc;
-  if ((rc = wsum.alloc(arena, sizeof(uint32_t) * 4 * WORDS * Wr * (2 + c)))) return rc;
-  const uint32_t* pts_internal = reinterpret_cast<const uint32_t*>(points_internal);
-  const uint32_t* offsets = plan.offsets;
-  DevBuf pfirst, plast;
   {
-    const uint32_t K = ctx->msm_slice ? (uint32_t)ctx->msm_slice : 64u;
-    const size_t nslices = (M + K - 1) / K;
-    if ((rc = pfirst.alloc(arena, sizeof(XYZZ<DF>) * nslices))) return rc;
-    if ((rc = plast.alloc(arena, sizeof(XYZZ<DF>) * nslices))) return rc;
-    GM_HIP(hipMemsetAsync(buckets.p, 0, sizeof(XYZZ<DF>) * (size_t)total, st));  // all-zero XYZZ = infinity
+    GM_HIP(hipMemsetAsync(buckets.p, 0, sizeof(XYZZ<DF>) * (size_t)t.total, st));  // all-zero XYZZ = infinity
     ProfScope ps(ctx, G2 ? "msm_accum_g2" : "msm_accum_g1");
     // GM_MSM_ACCUM=prefetch|noprefetch overrides the per-group default (tuning)
     static const char* ov = getenv("GM_MSM_ACCUM");
@@ -639,115 +709,81 @@ int msm_run(gm_ctx* ctx, const MsmPlan& plan, const void* points_internal,
     if (ov && !strcmp(ov, "prefetch")) noprefetch = false;
     if (ov && !strcmp(ov, "noprefetch")) noprefetch = true;
     auto accum = noprefetch ? k_msm_accum_seg_g2<DF> : k_msm_accum_seg<DF>;
-    hipLaunchKernelGGL(accum, dim3(blocks_for(nslices, 128)), dim3(128), 0, st, pts_internal,
-                       (uint32_t)plan.npts, plan.keys, plan.vals, offsets, total, K, buckets.as<XYZZ<DF>>(),
-                       pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>(), errw.as<uint32_t>());
-    hipLaunchKernelGGL(k_msm_fixup<DF>, dim3(blocks_for(total, 128)), dim3(128), 0, st, offsets, total, K,
+    hipLaunchKernelGGL(accum, dim3(blocks_for(nslices, 128)), dim3(128), 0, st,
+                       reinterpret_cast<const uint32_t*>(points_internal), (uint32_t)plan.npts, plan.keys, plan.vals,
+                       plan.offsets, t.total, t.K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(),
+                       plast.as<XYZZ<DF>>(), errw.as<uint32_t>());
+    hipLaunchKernelGGL(k_msm_fixup<DF>, dim3(blocks_for(t.total, 128)), dim3(128), 0, st, plan.offsets, t.total, t.K,
                        buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>(),
                        errw.as<uint32_t>() + 1);
   }
   // Bucket reduction, launched speculatively: buckets spanning more than
   // FIX_SERIAL slices (skewed scalars) are only known once errw[1] (max span)
   // reaches the host, so the reduction is queued right away and redone after the
-  // long-span fixup in that (rare) case -- one host round trip per MSM instead of two.
-  uint32_t Q = 2;  // points per node: [G, U, Y_0..Y_{Q-3}]
-  XYZZ<DF>* cur = nullptr;
-  auto reduce = [&]() -> int {
-    ProfScope ps(ctx, "msm_bucket_reduce");
-    Q = 2;
-    hipLaunchKernelGGL(k_msm_seg<DF>, dim3(blocks_for((size_t)Wr * nseg, 128)), dim3(128), 0, st,
-                       buckets.as<XYZZ<DF>>(), nb, L, nseg, Wr, nodes_a.as<XYZZ<DF>>());
-    // LDS tree levels until one node per window
-    constexpr size_t SLOT_BUDGET = (96u << 10) / sizeof(XYZZ<DF>);
-    uint32_t m = nseg;
-    cur = nodes_a.as<XYZZ<DF>>();
-    XYZZ<DF>* nxt = nodes_b.as<XYZZ<DF>>();
-    while (m > 1) {
-      uint32_t lg = 0;
-      // largest power-of-two group with NT*Q slots in budget and <= 2 tasks per thread
-      while ((2u << lg) <= m && (size_t)(2u << lg) * Q <= SLOT_BUDGET && (1u << lg) * (Q + 1) <= 2 * BS_THREADS) lg++;
-      if (lg == 0) {
-        set_error("msm: bucket reduction does not fit LDS");
-        return GM_ERR_INVALID;
-      }
-      const uint32_t NT = 1u << lg;
-      const uint32_t groups = m / NT;
-      hipLaunchKernelGGL(k_msm_bitsum<DF>, dim3(Wr * groups), dim3(BS_THREADS), sizeof(XYZZ<DF>) * NT * Q, st, cur, m,
-                         Q, NT, lg, nxt);
-      Q += lg;
-      m = groups;
-      std::swap(cur, nxt);
-    }
-    hipLaunchKernelGGL(k_msm_export<DF>, dim3(blocks_for((size_t)Wr * Q, 128)), dim3(128), 0, st, cur, Wr * Q,
-                       wsum.as<uint32_t>());
-    GM_HIP(hipGetLastError());
-    return GM_OK;
-  };
-  static_assert(sizeof(HF) == 4 * WORDS, "host/device layout mismatch");
-  uint8_t* stage = nullptr;
-  auto readback = [&]() -> int {
-    const size_t wbytes = sizeof(uint32_t) * 4 * WORDS * Wr * Q;
-    void* pb;
-    if (int r = pinned_buf(ctx, 16 + wbytes, &pb)) return r;
-    stage = reinterpret_cast<uint8_t*>(pb);
-    GM_HIP(hipMemcpyAsync(stage, errw.p, 16, hipMemcpyDeviceToHost, st));
-    GM_HIP(hipMemcpyAsync(stage + 16, wsum.p, wbytes, hipMemcpyDeviceToHost, st));
-    GM_HIP(hipStreamSynchronize(st));
-    return GM_OK;
-  };
-  // Speculate only when uniform scalars would give no long span: the fullest
-  // bucket is then a top-window digit (n / 2^top_bits entries; plus the other
-  // windows' share when buckets are shared).  Large MSMs whose top window is
-  // narrow (2^24: 1024-4096 entries per top digit) sync on max span first.
+  // long-span fixup in that (rare) case.  Speculate only when uniform scalars
+  // would give no long span: the fullest bucket is then a top-window digit
+  // (n / 2^top_bits entries; plus the other windows' share when buckets are
+  // shared).  Large MSMs whose top window is narrow (2^24: 1024-4096 entries per
+  // top digit) sync on the max span first.
   {
-    const uint32_t K = ctx->msm_slice ? (uint32_t)ctx->msm_slice : 64u;
-    const int top_bits = C::FR_BITS - (int)(c * (plan.W - 1));
+    const int top_bits = C::FR_BITS - (int)(t.c * (t.W - 1));
     double fullest = (double)plan.n / std::ldexp(1.0, top_bits > 0 ? top_bits : 0);
-    if (Wr == 1 && plan.W > 1) fullest += (double)(plan.W - 1) * (double)plan.n / (double)nb;
-    if (fullest > 0.5 * FIX_SERIAL * K) {
-      void* pb;
-      if ((rc = pinned_buf(ctx, 16, &pb))) return rc;
+    if (t.Wr == 1 && t.W > 1) fullest += (double)(t.W - 1) * (double)plan.n / (double)t.nb;
+    if (fullest > 0.5 * FIX_SERIAL * t.K) {
+      uint8_t* pb;
+      if ((rc = tail_pinned_buf(ctx, 16, &pb))) return rc;
       GM_HIP(hipMemcpyAsync(pb, errw.p, 16, hipMemcpyDeviceToHost, st));
       GM_HIP(hipStreamSynchronize(st));
       uint32_t ms;
-      memcpy(&ms, (uint8_t*)pb + 4, 4);
+      memcpy(&ms, pb + 4, 4);
       if (ms > FIX_SERIAL) {
-        const size_t nslices = (M + K - 1) / K;
-        for (uint32_t d = 0; (1u << d) < ms; d++)
-          hipLaunchKernelGGL(k_msm_fix_tree<DF>, dim3(blocks_for(nslices, 128)), dim3(128), 0, st, plan.keys,
-                             offsets, total, K, (uint32_t)nslices, d, pfirst.as<XYZZ<DF>>());
-        hipLaunchKernelGGL(k_msm_fixup_long<DF>, dim3(blocks_for(total, 128)), dim3(128), 0, st, offsets, total,
-                           K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>());
+        if ((rc = msm_fix_long<C, G2>(ctx, t, ms))) return rc;
         GM_HIP(hipMemsetAsync(errw.as<uint32_t>() + 1, 0, 4, st));  // long spans resolved
       }
     }
   }
-  if ((rc = reduce()) || (rc = readback())) return rc;
+  if ((rc = msm_reduce<C, G2>(ctx, t))) return rc;
+  return msm_readback<C, G2>(ctx, t);
+}
+
+// Host tail of a launched MSM: waits for its readback (not for the stream),
+// redoes the reduction after a tree fixup if a long span showed up, then the
+// host Horner over the window / bit-position nodes.
+template <class C, bool G2>
+int msm_finish(gm_ctx* ctx, MsmTail& t, typename GroupSel<C, G2>::HF (&jac_out)[3]) {
+  using HF = typename GroupSel<C, G2>::HF;
+  using HJ = host::Jac<HF>;
+  if (t.n == 0) {
+    HJ inf = HJ::inf();
+    jac_out[0] = inf.x;
+    jac_out[1] = inf.y;
+    jac_out[2] = inf.z;
+    return GM_OK;
+  }
+  int rc;
+  GM_HIP(hipEventSynchronize(t.done));
   uint32_t herr, maxspan;
-  memcpy(&herr, stage, 4);
-  memcpy(&maxspan, stage + 4, 4);
+  memcpy(&herr, t.stage, 4);
+  memcpy(&maxspan, t.stage + 4, 4);
   if (maxspan > FIX_SERIAL) {
-    const uint32_t K = ctx->msm_slice ? (uint32_t)ctx->msm_slice : 64u;
-    const size_t nslices = (M + K - 1) / K;
-    for (uint32_t d = 0; (1u << d) < maxspan; d++)
-      hipLaunchKernelGGL(k_msm_fix_tree<DF>, dim3(blocks_for(nslices, 128)), dim3(128), 0, st, plan.keys,
-                         offsets, total, K, (uint32_t)nslices, d, pfirst.as<XYZZ<DF>>());
-    hipLaunchKernelGGL(k_msm_fixup_long<DF>, dim3(blocks_for(total, 128)), dim3(128), 0, st, offsets, total, K,
-                       buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>());
-    if ((rc = reduce()) || (rc = readback())) return rc;
-    memcpy(&herr, stage, 4);
+    if ((rc = msm_fix_long<C, G2>(ctx, t, maxspan)) || (rc = msm_reduce<C, G2>(ctx, t)) ||
+        (rc = msm_readback<C, G2>(ctx, t)))
+      return rc;
+    GM_HIP(hipEventSynchronize(t.done));
+    memcpy(&herr, t.stage, 4);
   }
   if (herr) {
     set_error("msm: internal consistency check failed (code " + std::to_string(herr) + ")");
     return GM_ERR_DEVICE;
   }
+  const uint32_t Wr = t.Wr, Q = t.Q, c = t.c;
   std::vector<HF> hw(4 * (size_t)Wr * Q);
-  memcpy(hw.data(), stage + 16, sizeof(HF) * hw.size());
+  memcpy(hw.data(), t.stage + 16, sizeof(HF) * hw.size());
   // Host Horner over bit positions: window w contributes U_w at 2^(c w) and
   // Y_{w,b} at 2^(c w + log2 L + b) (b < Q - 2 = log2(nseg), so every exponent
   // stays below c (w + 1)).  Shared buckets: one window, w = 0.
   uint32_t lgL = 0;
-  while ((1u << lgL) < L) lgL++;
+  while ((1u << lgL) < t.L) lgL++;
   const int top = (int)(c * Wr);
   std::vector<std::vector<uint32_t>> at(top + 1);  // point ids per exponent
   for (uint32_t w = 0; w < Wr; w++) {
@@ -770,10 +806,18 @@ int msm_run(gm_ctx* ctx, const MsmPlan& plan, const void* points_internal,
 }
 
 template <class C, bool G2>
-int msm_device(gm_ctx* ctx, const void* scalars_dev, const void* points_dev, size_t n,
-               typename GroupSel<C, G2>::HF (&jac_out)[3], bool points_internal, const MsmPrecomp* pre) {
-  using DF = typename GroupSel<C, G2>::DF;
+int msm_run(gm_ctx* ctx, const MsmPlan& plan, const void* points_internal,
+            typename GroupSel<C, G2>::HF (&jac_out)[3]) {
   Arena arena(ctx);
+  MsmTail t;
+  int rc = msm_launch<C, G2>(ctx, arena, plan, points_internal, t);
+  return rc ? rc : msm_finish<C, G2>(ctx, t, jac_out);
+}
+
+template <class C, bool G2>
+int msm_device_launch(gm_ctx* ctx, Arena& arena, const void* scalars_dev, const void* points_dev, size_t n,
+                      bool points_internal, const MsmPrecomp* pre, MsmTail& t) {
+  using DF = typename GroupSel<C, G2>::DF;
   int rc;
   const void* pts = points_dev;
   DevBuf ipts;
@@ -790,7 +834,16 @@ int msm_device(gm_ctx* ctx, const void* scalars_dev, const void* points_dev, siz
   }
   MsmPlan plan;
   if ((rc = msm_plan<C>(ctx, arena, scalars_dev, n, pre, plan))) return rc;
-  return msm_run<C, G2>(ctx, plan, pts, jac_out);
+  return msm_launch<C, G2>(ctx, arena, plan, pts, t);
+}
+
+template <class C, bool G2>
+int msm_device(gm_ctx* ctx, const void* scalars_dev, const void* points_dev, size_t n,
+               typename GroupSel<C, G2>::HF (&jac_out)[3], bool points_internal, const MsmPrecomp* pre) {
+  Arena arena(ctx);
+  MsmTail t;
+  int rc = msm_device_launch<C, G2>(ctx, arena, scalars_dev, points_dev, n, points_internal, pre, t);
+  return rc ? rc : msm_finish<C, G2>(ctx, t, jac_out);
 }
 
 template <class C, bool G2>
@@ -833,6 +886,10 @@ int msm_precompute_points(gm_ctx* ctx, const void* gnark_points, size_t n, const
   template int msm_prepare_points<C, G2>(gm_ctx*, const void*, size_t, void*);                \
   template int msm_precompute_points<C, G2>(gm_ctx*, const void*, size_t, const MsmPrecomp&, void*); \
   template int msm_run<C, G2>(gm_ctx*, const MsmPlan&, const void*, typename GroupSel<C, G2>::HF (&)[3]); \
+  template int msm_launch<C, G2>(gm_ctx*, Arena&, const MsmPlan&, const void*, MsmTail&);      \
+  template int msm_finish<C, G2>(gm_ctx*, MsmTail&, typename GroupSel<C, G2>::HF (&)[3]);     \
+  template int msm_device_launch<C, G2>(gm_ctx*, Arena&, const void*, const void*, size_t, bool, \
+                                        const MsmPrecomp*, MsmTail&);                          \
   template int msm_device<C, G2>(gm_ctx*, const void*, const void*, size_t,                    \
                                  typename GroupSel<C, G2>::HF (&)[3], bool, const MsmPrecomp*);
 #define GM_MSM_INSTANTIATE_PLAN(C) \

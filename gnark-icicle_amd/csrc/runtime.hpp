@@ -31,6 +31,16 @@ struct KernelStat {
   uint64_t count = 0;
 };
 
+// One bump-allocated workspace: chunks of hipMalloc'd memory (see Arena).
+struct ArenaState {
+  struct Chunk {
+    char* base;
+    size_t cap;
+  };
+  std::vector<Chunk> chunks;
+  size_t cur_chunk = 0, cur_top = 0;
+};
+
 }  // namespace gm
 
 struct gm_ctx {
@@ -55,13 +65,14 @@ struct gm_ctx {
   std::map<int, void*> ntt_domains;
   int msm_c_override = 0;
   int msm_slice = 0;  // entries per thread in the bucket accumulation (0 = default)
-  // workspace arena: chunks of hipMalloc'd memory, stack-discipline scopes
-  struct Chunk {
-    char* base;
-    size_t cap;
-  };
-  std::vector<Chunk> chunks;
-  size_t cur_chunk = 0, cur_top = 0;
+  // workspace arena (stack-discipline scopes), plus two more for MSMs whose host
+  // tail is deferred (pipelined MSMs: gm_msm_async, the Groth16 MSM sequence)
+  gm::ArenaState arena;
+  gm::ArenaState slots[2];
+  bool slot_busy[2] = {false, false};
+  // pinned readback buffers of deferred MSM tails (rotating)
+  void* tail_pinned[4] = {nullptr, nullptr, nullptr, nullptr};
+  int tail_next = 0;
 };
 
 namespace gm {
@@ -116,29 +127,31 @@ inline void prof_collect(gm_ctx* ctx) {
 // stream-synchronous, so a released range is never still in use by a kernel.
 struct Arena {
   gm_ctx* ctx;
+  ArenaState* st;
   size_t saved_chunk, saved_top;
-  explicit Arena(gm_ctx* c) : ctx(c), saved_chunk(c->cur_chunk), saved_top(c->cur_top) {}
+  explicit Arena(gm_ctx* c, ArenaState* s = nullptr)
+      : ctx(c), st(s ? s : &c->arena), saved_chunk(st->cur_chunk), saved_top(st->cur_top) {}
   ~Arena() {
-    ctx->cur_chunk = saved_chunk;
-    ctx->cur_top = saved_top;
+    st->cur_chunk = saved_chunk;
+    st->cur_top = saved_top;
   }
   Arena(const Arena&) = delete;
   Arena& operator=(const Arena&) = delete;
   int alloc(size_t bytes, void** out) {
     bytes = (bytes + 255) & ~size_t(255);
     if (bytes == 0) bytes = 256;
-    while (ctx->cur_chunk < ctx->chunks.size()) {
-      auto& ch = ctx->chunks[ctx->cur_chunk];
-      if (ctx->cur_top + bytes <= ch.cap) {
-        *out = ch.base + ctx->cur_top;
-        ctx->cur_top += bytes;
+    while (st->cur_chunk < st->chunks.size()) {
+      auto& ch = st->chunks[st->cur_chunk];
+      if (st->cur_top + bytes <= ch.cap) {
+        *out = ch.base + st->cur_top;
+        st->cur_top += bytes;
         return GM_OK;
       }
-      ctx->cur_chunk++;
-      ctx->cur_top = 0;
+      st->cur_chunk++;
+      st->cur_top = 0;
     }
     size_t cap = bytes;
-    size_t last = ctx->chunks.empty() ? 0 : ctx->chunks.back().cap;
+    size_t last = st->chunks.empty() ? 0 : st->chunks.back().cap;
     if (cap < 2 * last) cap = 2 * last;
     if (cap < (size_t(64) << 20)) cap = size_t(64) << 20;
     void* p = nullptr;
@@ -152,13 +165,63 @@ struct Arena {
         return GM_ERR_OOM;
       }
     }
-    ctx->chunks.push_back({(char*)p, cap});
-    ctx->cur_chunk = ctx->chunks.size() - 1;
-    ctx->cur_top = bytes;
+    st->chunks.push_back({(char*)p, cap});
+    st->cur_chunk = st->chunks.size() - 1;
+    st->cur_top = bytes;
     *out = p;
     return GM_OK;
   }
 };
+
+// A deferred-tail arena slot of the context (at most two MSMs in flight).
+struct SlotArena {
+  gm_ctx* ctx;
+  int k = -1;
+  Arena* a = nullptr;
+  int take() {
+    for (int i = 0; i < 2; i++)
+      if (!ctx->slot_busy[i]) {
+        k = i;
+        ctx->slot_busy[i] = true;
+        a = new Arena(ctx, &ctx->slots[i]);
+        return GM_OK;
+      }
+    set_error("at most two MSMs may be in flight per context");
+    return GM_ERR_INVALID;
+  }
+  void release() {
+    if (a) {
+      delete a;
+      a = nullptr;
+      ctx->slot_busy[k] = false;
+    }
+  }
+  explicit SlotArena(gm_ctx* c) : ctx(c) {}
+  ~SlotArena() { release(); }
+  SlotArena(const SlotArena&) = delete;
+  SlotArena& operator=(const SlotArena&) = delete;
+};
+
+// Pinned readback buffer of a deferred MSM tail (4 rotating 512 KiB buffers).
+inline int tail_pinned_buf(gm_ctx* ctx, size_t bytes, uint8_t** out) {
+  constexpr size_t CAP = size_t(512) << 10;
+  if (bytes > CAP) {
+    set_error("msm: readback larger than the tail buffer");
+    return GM_ERR_INVALID;
+  }
+  void*& b = ctx->tail_pinned[ctx->tail_next];
+  ctx->tail_next = (ctx->tail_next + 1) & 3;
+  if (!b) {
+    hipError_t e = hipHostMalloc(&b, CAP, hipHostMallocDefault);
+    if (e != hipSuccess) {
+      b = nullptr;
+      set_error(std::string("hipHostMalloc: ") + hipGetErrorString(e));
+      return GM_ERR_OOM;
+    }
+  }
+  *out = static_cast<uint8_t*>(b);
+  return GM_OK;
+}
 
 // Pinned host staging of at least `bytes` (grown on demand; freed by gm_destroy).
 inline int pinned_buf(gm_ctx* ctx, size_t bytes, void** out) {

@@ -53,7 +53,7 @@ SYMBOLS = [
     "gm_multi_context", "gm_g16_pk_upload_multi", "gm_g16_pk_free_multi", "gm_g16_prove_multi",
     "gm_g16_pk_upload_dump", "gm_g16_pk_upload_dump_shard", "gm_g16_pk_save_cache", "gm_g16_pk_load_cache",
     "gm_g16_stage_begin", "gm_g16_stage_put_range", "gm_g16_stage_put_indexed", "gm_g16_stage_prove",
-    "gm_g16_stage_free",
+    "gm_g16_stage_free", "gm_msm_async", "gm_msm_wait",
 ]
 
 
@@ -139,6 +139,8 @@ def load_library(path: str = LIB_PATH):
     L.gm_g16_stage_put_indexed.argtypes = [vp, i, vp, vp, sz]
     L.gm_g16_stage_prove.argtypes = [vp, vp, vp, vp, vp, vp]
     L.gm_g16_stage_free.argtypes = [vp]
+    L.gm_msm_async.argtypes = [vp, i, i, vp, vp, sz, pvp]
+    L.gm_msm_wait.argtypes = [vp, vp, vp]
     _lib = L
     return L
 
@@ -291,6 +293,15 @@ class Context:
         pp = points.ptr if isinstance(points, DeviceBuffer) else points
         _check(load_library().gm_msm(self.handle, curve_id(curve), int(g2), sp, pp, n, _p(jac), _p(aff)))
         return jac.tobytes(), aff.tobytes()
+
+    def msm_async(self, curve, scalars: DeviceBuffer, points: DeviceBuffer, n: int, g2: bool = False):
+        """Queues an MSM (gm_msm_async); .wait() returns (jacobian_bytes, affine_bytes).
+        At most two in flight per context, waited in issue order."""
+        h = ctypes.c_void_p()
+        sp = scalars.ptr if isinstance(scalars, DeviceBuffer) else scalars
+        pp = points.ptr if isinstance(points, DeviceBuffer) else points
+        _check(load_library().gm_msm_async(self.handle, curve_id(curve), int(g2), sp, pp, n, ctypes.byref(h)))
+        return PendingMsm(h, curve, g2)
 
     def points_upload(self, curve, points, g2: bool = False) -> DeviceBuffer:
         """Device-resident point set in the MSM's internal layout (pk arrays, SRS)."""
@@ -678,6 +689,18 @@ class ProvingKey:
         _check(load_library().gm_g16_prove_partial(self.ctx.handle, self.handle, wires.ptr, a.ptr, b.ptr, c.ptr,
                                                    nb_constraints, _p(out)))
         return out.tobytes()
+
+
+class PendingMsm:
+    def __init__(self, handle, curve, g2):
+        self.handle, self.curve, self.g2 = handle, curve, g2
+
+    def wait(self):
+        jac = np.zeros(jac_bytes(self.curve, self.g2), np.uint8)
+        aff = np.zeros(point_bytes(self.curve, self.g2), np.uint8)
+        h, self.handle = self.handle, None
+        _check(load_library().gm_msm_wait(h, _p(jac), _p(aff)))
+        return jac.tobytes(), aff.tobytes()
 
 
 class Stage:

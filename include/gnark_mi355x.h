@@ -83,6 +83,15 @@ int gm_copy_points_to_device(gm_ctx* ctx, int curve, int g2, const void* host_po
 int gm_msm(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const void* points_dev,
            size_t n, void* out_jac, void* out_affine);
 /* Same with scalars in host memory (copied on the context stream). */
+/* Pipelined MSM: gm_msm_async queues the device work of gm_msm (same
+ * arguments) and returns at once; gm_msm_wait finishes it (host tail: checks
+ * and the Horner combination) and frees the handle.  The host tail of one MSM
+ * thus overlaps the device work of the next one issued before it.  At most two
+ * MSMs may be in flight per context; wait in issue order. */
+typedef struct gm_msm_pending gm_msm_pending;
+int gm_msm_async(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const void* points_dev, size_t n,
+                 gm_msm_pending** out);
+int gm_msm_wait(gm_msm_pending* pending, void* out_jacobian, void* out_affine);
 int gm_msm_host_scalars(gm_ctx* ctx, int curve, int g2, const void* scalars_host,
                         const void* points_dev, size_t n, void* out_jac, void* out_affine);
 

@@ -403,3 +403,32 @@ def test_msm_three_level_sort_skewed(gm_ctx, oracle, monkeypatch):
     finally:
         for b in (S, K, P):
             b.free()
+
+
+def test_msm_async_pipelined(gm_ctx, oracle):
+    """gm_msm_async / gm_msm_wait: two MSMs in flight (different curves, groups
+    and sizes), waited in order, equal the oracle; a third in flight is refused."""
+    import gnark_mi355x as gm
+    cases = []
+    for cname, g2, n in (("bn254", False, 5000), ("bls12377", True, 777), ("bn254", True, 3000)):
+        S = gm_ctx.random_scalars(cname, n, seed=0xA5A5 + n)
+        K = gm_ctx.random_scalars(cname, n, seed=0x5A5A + n)
+        P = gm_ctx.batch_mul_base(cname, g2, gm.generator(cname, g2), K, n)
+        K.free()
+        cases.append((cname, g2, n, S, P, oracle.msm(cname, g2, S.to_host(), P.to_host())))
+    try:
+        pend = []
+        for k, (cname, g2, n, S, P, exp) in enumerate(cases):
+            pend.append(gm_ctx.msm_async(cname, S, P, n, g2))
+            if k >= 1:
+                assert pend[k - 1].wait()[1] == cases[k - 1][5]
+        assert pend[-1].wait()[1] == cases[-1][5]
+        a = gm_ctx.msm_async("bn254", cases[0][3], cases[0][4], cases[0][2])
+        b = gm_ctx.msm_async("bn254", cases[0][3], cases[0][4], cases[0][2])
+        with pytest.raises(gm.GmError, match="in flight"):
+            gm_ctx.msm_async("bn254", cases[0][3], cases[0][4], cases[0][2])
+        assert a.wait()[1] == cases[0][5] and b.wait()[1] == cases[0][5]
+    finally:
+        for c in cases:
+            c[3].free()
+            c[4].free()
