@@ -542,8 +542,9 @@ int msm_plan(gm_ctx* ctx, Arena& arena, const void* scalars_dev, size_t n, const
   const char* ming = getenv("GM_MSM_SORT_MING");
   sg.G = ming ? (uint32_t)std::min(10, std::max(0, atoi(ming))) : 0u;
   // (shared layout at 2^20: 8192 pass-1 bins with G = 0 measured 0.285 ms vs
-  // 0.315 with the middle pass, so only the plain layout uses the 512 rule)
-  const uint32_t max_touched = shared ? 8192u : 512u;
+  // 0.315 with the middle pass -- its 109 MB of entries stay in the caches, which
+  // merge the short write runs; at 2^24, 1.6 GB, they do not: 2.4 ms per sort)
+  const uint32_t max_touched = (shared && M < (size_t(1) << 24)) ? 8192u : 512u;
   while (sg.G < 10 && (touched(sg.F + sg.G) > max_touched || bins(sg.F + sg.G) > 8192)) sg.G++;
   while (sg.G && sg.F + sg.G > 31) sg.G--;
   sg.NC = bins(sg.F);
@@ -675,9 +676,13 @@ int msm_launch(gm_ctx* ctx, Arena& arena, const MsmPlan& plan, const void* point
   // level-1 segment length (buckets).  Measured at 2^20 (BN254 G1 / G2 /
   // BLS12-377 G2 reduction ms): L = 1: 0.83 / 4.2 / 16.9, L = 2: 0.51 / 2.6 / 9.6,
   // L = 4: 0.36 / 1.74 / 6.05 -- the LDS bit-sum trees cost more per add than the
-  // running sums.  GM_MSM_SEGL overrides (tuning).
+  // running sums.  So L grows (to 32) as long as k_msm_seg keeps >= 128K threads
+  // (two waves per SIMD): 4 for 2^20 plain, 16 for the one-window 2^21 buckets
+  // of a precomputed 2^24 key.  GM_MSM_SEGL overrides (tuning).
   static const int segl_env = getenv("GM_MSM_SEGL") ? atoi(getenv("GM_MSM_SEGL")) : 0;
-  const uint32_t Lwant = segl_env > 0 ? (uint32_t)segl_env : 4u;
+  uint32_t Lwant = 4;
+  while (Lwant < 32 && (size_t)t.Wr * t.nb / (2 * Lwant) >= (size_t(1) << 17)) Lwant *= 2;
+  if (segl_env > 0) Lwant = (uint32_t)segl_env;
   t.L = t.nb >= Lwant ? Lwant : t.nb;
   t.nseg = t.nb / t.L;
   t.K = ctx->msm_slice ? (uint32_t)ctx->msm_slice : 64u;
@@ -713,6 +718,9 @@ int msm_launch(gm_ctx* ctx, Arena& arena, const MsmPlan& plan, const void* point
                        reinterpret_cast<const uint32_t*>(points_internal), (uint32_t)plan.npts, plan.keys, plan.vals,
                        plan.offsets, t.total, t.K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(),
                        plast.as<XYZZ<DF>>(), errw.as<uint32_t>());
+  }
+  {
+    ProfScope ps(ctx, "msm_fixup");
     hipLaunchKernelGGL(k_msm_fixup<DF>, dim3(blocks_for(t.total, 128)), dim3(128), 0, st, plan.offsets, t.total, t.K,
                        buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>(),
                        errw.as<uint32_t>() + 1);
