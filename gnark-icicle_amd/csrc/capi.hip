@@ -167,6 +167,11 @@ int gm_destroy(gm_ctx* ctx) {
     hipEventDestroy(p.a);
     hipEventDestroy(p.b);
   }
+  for (hipStream_t s : ctx->slot_stream)
+    if (s) {
+      hipStreamSynchronize(s);
+      hipStreamDestroy(s);
+    }
   hipStreamDestroy(ctx->stream);
   if (ctx->aux) hipStreamDestroy(ctx->aux);
   if (ctx->copy) hipStreamDestroy(ctx->copy);
@@ -302,12 +307,20 @@ int gm_msm(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const void* 
 struct gm_msm_pending {
   gm_ctx* ctx;
   int curve, g2;
+  hipStream_t st = nullptr;  // stream the MSM runs on (slot stream or ctx->stream)
   gm::SlotArena slot;
   gm::MsmTail tail;
   explicit gm_msm_pending(gm_ctx* c) : ctx(c), slot(c) {}
 };
 
 namespace {
+// ctx->stream temporarily replaced (all MSM code queues on ctx->stream)
+struct StreamSwap {
+  gm_ctx* ctx;
+  hipStream_t old;
+  StreamSwap(gm_ctx* c, hipStream_t s) : ctx(c), old(c->stream) { c->stream = s; }
+  ~StreamSwap() { ctx->stream = old; }
+};
 template <class C, bool G2>
 int msm_wait_t(gm_msm_pending* p, void* out_jac, void* out_aff) {
   using HF = typename GroupSel<C, G2>::HF;
@@ -335,6 +348,21 @@ int gm_msm_async(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const 
   p->curve = curve;
   p->g2 = g2 ? 1 : 0;
   int rc = p->slot.take();
+  // Slot stream (GM_MSM_SLOT_STREAMS=0: everything on ctx->stream, A/B).  It
+  // starts after the work already queued on ctx->stream (the inputs).
+  static const bool slot_streams = !(getenv("GM_MSM_SLOT_STREAMS") && !strcmp(getenv("GM_MSM_SLOT_STREAMS"), "0"));
+  p->st = ctx->stream;
+  if (rc == GM_OK && slot_streams) {
+    hipStream_t& ss = ctx->slot_stream[p->slot.k];
+    if (!ss) GM_HIP(hipStreamCreateWithFlags(&ss, hipStreamNonBlocking));
+    hipEvent_t ev;
+    GM_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    GM_HIP(hipEventRecord(ev, ctx->stream));
+    GM_HIP(hipStreamWaitEvent(ss, ev, 0));
+    GM_HIP(hipEventDestroy(ev));
+    p->st = ss;
+  }
+  StreamSwap sw(ctx, p->st);
   if (rc == GM_OK) {
     Arena& a = *p->slot.a;
     if (curve == GM_BN254)
@@ -358,6 +386,7 @@ int gm_msm_wait(gm_msm_pending* p, void* out_jac, void* out_affine) {
   std::lock_guard<std::recursive_mutex> g(ctx->mu);
   GM_HIP(hipSetDevice(ctx->device));
   int rc;
+  StreamSwap sw(ctx, p->st);  // a long-span redo runs on the MSM's own stream
   if (p->curve == GM_BN254)
     rc = p->g2 ? msm_wait_t<CurveBN254, true>(p, out_jac, out_affine) : msm_wait_t<CurveBN254, false>(p, out_jac, out_affine);
   else

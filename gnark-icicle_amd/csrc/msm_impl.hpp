@@ -25,6 +25,7 @@
 // Exact group arithmetic: the result is independent of summation order.
 #include "curves.hpp"
 #include "msm.hpp"
+#include "pair_fp2.hpp"
 #include "runtime.hpp"
 
 #include <cmath>
@@ -309,6 +310,29 @@ k_msm_accum_seg_g2(const uint32_t* __restrict__ points, uint32_t n, const uint32
                    uint32_t K, XYZZ<F>* __restrict__ buckets, XYZZ<F>* __restrict__ part_first,
                    XYZZ<F>* __restrict__ part_last, uint32_t* __restrict__ err) {
   accum_seg_body<F, false>(points, n, keys, vals, offsets, total, K, buckets, part_first, part_last, err);
+}
+
+// G2 default: Fp2 components split across lane pairs (pair_fp2.hpp).
+template <class F>
+struct PairSel {
+  static constexpr bool ok = false;
+};
+template <class P, int B>
+struct PairSel<Fe2<P, B>> {
+  static constexpr bool ok = true;
+  static constexpr auto kernel() { return k_msm_accum_seg_pair<P, B>; }
+  static constexpr auto fixup() { return k_msm_fixup_pair<P, B>; }
+  static constexpr auto fix_tree() { return k_msm_fix_tree_pair<P, B>; }
+  static constexpr auto fixup_long() { return k_msm_fixup_long_pair<P, B>; }
+  static constexpr auto seg() { return k_msm_seg_pair<P, B>; }
+  static constexpr auto bitsum() { return k_msm_bitsum_pair<P, B>; }
+};
+// G2 runs on lane pairs unless GM_MSM_ACCUM=prefetch|noprefetch asks for the
+// one-lane kernels (A/B)
+inline bool g2_pairs() {
+  static const char* ov = getenv("GM_MSM_ACCUM");
+  static const bool on = !(ov && (!strcmp(ov, "prefetch") || !strcmp(ov, "noprefetch")));
+  return on;
 }
 
 // Merge the partial sums of buckets cut by slice edges.  Bucket b spans slices
@@ -596,8 +620,16 @@ int msm_reduce(gm_ctx* ctx, MsmTail& t) {
   hipStream_t st = ctx->stream;
   ProfScope ps(ctx, "msm_bucket_reduce");
   uint32_t Q = 2;  // points per node: [G, U, Y_0..Y_{Q-3}]
-  hipLaunchKernelGGL(k_msm_seg<DF>, dim3(blocks_for((size_t)t.Wr * t.nseg, 128)), dim3(128), 0, st,
-                     (const XYZZ<DF>*)t.buckets, t.nb, t.L, t.nseg, t.Wr, (XYZZ<DF>*)t.nodes_a);
+  bool pairs = false;
+  if constexpr (PairSel<DF>::ok) pairs = g2_pairs();
+  if constexpr (PairSel<DF>::ok) {
+    if (pairs)
+      hipLaunchKernelGGL(PairSel<DF>::seg(), dim3(blocks_for(2 * (size_t)t.Wr * t.nseg, 128)), dim3(128), 0, st,
+                         (const uint32_t*)t.buckets, t.nb, t.L, t.nseg, t.Wr, (uint32_t*)t.nodes_a);
+  }
+  if (!pairs)
+    hipLaunchKernelGGL(k_msm_seg<DF>, dim3(blocks_for((size_t)t.Wr * t.nseg, 128)), dim3(128), 0, st,
+                       (const XYZZ<DF>*)t.buckets, t.nb, t.L, t.nseg, t.Wr, (XYZZ<DF>*)t.nodes_a);
   // LDS tree levels until one node per window
   constexpr size_t SLOT_BUDGET = (96u << 10) / sizeof(XYZZ<DF>);
   uint32_t m = t.nseg;
@@ -613,8 +645,14 @@ int msm_reduce(gm_ctx* ctx, MsmTail& t) {
     }
     const uint32_t NT = 1u << lg;
     const uint32_t groups = m / NT;
-    hipLaunchKernelGGL(k_msm_bitsum<DF>, dim3(t.Wr * groups), dim3(BS_THREADS), sizeof(XYZZ<DF>) * NT * Q, st, cur,
-                       m, Q, NT, lg, nxt);
+    if constexpr (PairSel<DF>::ok) {
+      if (pairs)
+        hipLaunchKernelGGL(PairSel<DF>::bitsum(), dim3(t.Wr * groups), dim3(BS_PAIR_THREADS), sizeof(XYZZ<DF>) * NT * Q,
+                           st, (const uint32_t*)cur, m, Q, NT, lg, (uint32_t*)nxt);
+    }
+    if (!pairs)
+      hipLaunchKernelGGL(k_msm_bitsum<DF>, dim3(t.Wr * groups), dim3(BS_THREADS), sizeof(XYZZ<DF>) * NT * Q, st,
+                         cur, m, Q, NT, lg, nxt);
     Q += lg;
     m = groups;
     std::swap(cur, nxt);
@@ -632,6 +670,18 @@ int msm_fix_long(gm_ctx* ctx, MsmTail& t, uint32_t maxspan) {
   using DF = typename GroupSel<C, G2>::DF;
   hipStream_t st = ctx->stream;
   const size_t nslices = (t.M + t.K - 1) / t.K;
+  if constexpr (PairSel<DF>::ok) {
+    if (g2_pairs()) {
+      for (uint32_t d = 0; (1u << d) < maxspan; d++)
+        hipLaunchKernelGGL(PairSel<DF>::fix_tree(), dim3(blocks_for(2 * nslices, 128)), dim3(128), 0, st, t.keys,
+                           t.offsets, t.total, t.K, (uint32_t)nslices, d, (uint32_t*)t.pfirst, FIX_SERIAL);
+      hipLaunchKernelGGL(PairSel<DF>::fixup_long(), dim3(blocks_for(2 * (size_t)t.total, 128)), dim3(128), 0, st,
+                         t.offsets, t.total, t.K, (uint32_t*)t.buckets, (const uint32_t*)t.pfirst,
+                         (const uint32_t*)t.plast, FIX_SERIAL);
+      GM_HIP(hipGetLastError());
+      return GM_OK;
+    }
+  }
   for (uint32_t d = 0; (1u << d) < maxspan; d++)
     hipLaunchKernelGGL(k_msm_fix_tree<DF>, dim3(blocks_for(nslices, 128)), dim3(128), 0, st, t.keys, t.offsets,
                        t.total, t.K, (uint32_t)nslices, d, (XYZZ<DF>*)t.pfirst);
@@ -708,22 +758,46 @@ int msm_launch(gm_ctx* ctx, Arena& arena, const MsmPlan& plan, const void* point
   {
     GM_HIP(hipMemsetAsync(buckets.p, 0, sizeof(XYZZ<DF>) * (size_t)t.total, st));  // all-zero XYZZ = infinity
     ProfScope ps(ctx, G2 ? "msm_accum_g2" : "msm_accum_g1");
-    // GM_MSM_ACCUM=prefetch|noprefetch overrides the per-group default (tuning)
+    // G2 defaults to lane pairs; GM_MSM_ACCUM=prefetch|noprefetch selects the
+    // one-lane kernels instead (tuning / A-B)
     static const char* ov = getenv("GM_MSM_ACCUM");
+    bool pair = G2 && g2_pairs();
     bool noprefetch = G2;
     if (ov && !strcmp(ov, "prefetch")) noprefetch = false;
     if (ov && !strcmp(ov, "noprefetch")) noprefetch = true;
-    auto accum = noprefetch ? k_msm_accum_seg_g2<DF> : k_msm_accum_seg<DF>;
-    hipLaunchKernelGGL(accum, dim3(blocks_for(nslices, 128)), dim3(128), 0, st,
-                       reinterpret_cast<const uint32_t*>(points_internal), (uint32_t)plan.npts, plan.keys, plan.vals,
-                       plan.offsets, t.total, t.K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(),
-                       plast.as<XYZZ<DF>>(), errw.as<uint32_t>());
+    if constexpr (PairSel<DF>::ok) {
+      if (pair) {
+        hipLaunchKernelGGL(PairSel<DF>::kernel(), dim3(blocks_for(2 * nslices, 128)), dim3(128), 0, st,
+                           reinterpret_cast<const uint32_t*>(points_internal), (uint32_t)plan.npts, plan.keys,
+                           plan.vals, plan.offsets, t.total, t.K, buckets.as<uint32_t>(), pfirst.as<uint32_t>(),
+                           plast.as<uint32_t>(), errw.as<uint32_t>());
+      }
+    } else {
+      pair = false;
+    }
+    if (!pair) {
+      auto accum = noprefetch ? k_msm_accum_seg_g2<DF> : k_msm_accum_seg<DF>;
+      hipLaunchKernelGGL(accum, dim3(blocks_for(nslices, 128)), dim3(128), 0, st,
+                         reinterpret_cast<const uint32_t*>(points_internal), (uint32_t)plan.npts, plan.keys,
+                         plan.vals, plan.offsets, t.total, t.K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(),
+                         plast.as<XYZZ<DF>>(), errw.as<uint32_t>());
+    }
   }
   {
     ProfScope ps(ctx, "msm_fixup");
-    hipLaunchKernelGGL(k_msm_fixup<DF>, dim3(blocks_for(t.total, 128)), dim3(128), 0, st, plan.offsets, t.total, t.K,
-                       buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>(),
-                       errw.as<uint32_t>() + 1);
+    bool done = false;
+    if constexpr (PairSel<DF>::ok) {
+      if (g2_pairs()) {
+        hipLaunchKernelGGL(PairSel<DF>::fixup(), dim3(blocks_for(2 * (size_t)t.total, 128)), dim3(128), 0, st,
+                           plan.offsets, t.total, t.K, buckets.as<uint32_t>(), pfirst.as<uint32_t>(),
+                           plast.as<uint32_t>(), errw.as<uint32_t>() + 1, FIX_SERIAL);
+        done = true;
+      }
+    }
+    if (!done)
+      hipLaunchKernelGGL(k_msm_fixup<DF>, dim3(blocks_for(t.total, 128)), dim3(128), 0, st, plan.offsets, t.total,
+                         t.K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>(),
+                         errw.as<uint32_t>() + 1);
   }
   // Bucket reduction, launched speculatively: buckets spanning more than
   // FIX_SERIAL slices (skewed scalars) are only known once errw[1] (max span)

@@ -73,6 +73,10 @@ struct gm_ctx {
   // pinned readback buffers of deferred MSM tails (rotating)
   void* tail_pinned[4] = {nullptr, nullptr, nullptr, nullptr};
   int tail_next = 0;
+  // one stream per slot (gm_msm_async): two independent MSMs in flight overlap
+  // on the device -- one's sort / reduction (HBM / latency-bound) runs beside the
+  // other's accumulation (VALU-bound).  Created on first use.
+  hipStream_t slot_stream[2] = {nullptr, nullptr};
 };
 
 namespace gm {
