@@ -142,7 +142,9 @@ GM_DEV void xyzz_add_aff_lz(XYZZ<Fe<P>>& a, const Affine<Fe<P>>& p) {
   F Q = fe_mul_lz(a.x, PP);                          // < 2p
   a.zzz = fe_mul_lz(a.zzz, PPP);
   F X3 = fe_sub_lz<4>(fe_sub_lz<2>(fe_sqr_lz(R), PPP), fe_add_lz(Q, Q));  // < 8p
-  a.y = fe_sub_lz<2>(fe_mul_lz(R, fe_sub_lz<8>(Q, X3)), fe_mul_lz(a.y, PPP));  // R (<6p) * (<10p); < 4p
+  // R (< 6p) * (Q - X3 + 8p < 10p) - Y1 (< 4p) * PPP (< 2p), one reduction:
+  // < 60 p^2 / R' + 2p < 2.4p (x2 y2 = 8 p^2 < R' p as fe_mul2_redc needs)
+  a.y = fe_mul2_redc(R, fe_sub_lz<8>(Q, X3), a.y, PPP, true);
   a.x = X3;
 }
 // Lazily reduced a += p for G2 buckets (Fp2 coordinates).  Invariants: every

@@ -43,51 +43,6 @@ GM_DEV Fe<P> fe_select(bool c, const Fe<P>& a, const Fe<P>& b) {
   return r;
 }
 
-// Montgomery reduction of x1*y1 + (neg ? -1 : 1) * x2*y2 (radix 2^29 product
-// scanning, one 64-bit column accumulator): signed columns when neg (arithmetic
-// shifts), unsigned otherwise.  All inputs have normalised limbs; |column| stays
-// below 2^63 (N = 9: 2^62.2, N = 14: 2^62.8 signed, 2^63.4 unsigned).  With neg,
-// p is added to the result, which makes it non-negative for x2*y2 < p R'.
-// Output < x1*y1 / R' + p (+ p when neg).
-template <class P>
-GM_DEV Fe<P> fe_mul2_redc(const Fe<P>& x1, const Fe<P>& y1, const Fe<P>& x2, const Fe<P>& y2, bool neg) {
-  constexpr int N = P::N;
-  uint32_t m[N];
-  Fe<P> r;
-  uint64_t acc = 0;
-#pragma unroll
-  for (int k = 0; k < 2 * N - 1; k++) {
-    uint64_t c1 = 0, c2 = 0;
-#pragma unroll
-    for (int i = (k - N + 1 > 0 ? k - N + 1 : 0); i <= (k < N - 1 ? k : N - 1); i++) {
-      c1 += (uint64_t)x1.v[i] * y1.v[k - i];
-      c2 += (uint64_t)x2.v[i] * y2.v[k - i];
-    }
-    acc += c1 + (neg ? (uint64_t)0 - c2 : c2);
-#pragma unroll
-    for (int i = (k - N + 1 > 0 ? k - N + 1 : 0); i <= (k - 1 < N - 1 ? k - 1 : N - 1); i++)
-      acc += (uint64_t)m[i] * P::p(k - i);
-    if (k < N) {
-      m[k] = ((uint32_t)acc * P::INV) & LIMB_MASK;
-      acc += (uint64_t)m[k] * P::p(0);
-    } else {
-      r.v[k - N] = (uint32_t)acc & LIMB_MASK;
-    }
-    acc = neg ? (uint64_t)((int64_t)acc >> RADIX) : acc >> RADIX;
-  }
-  r.v[N - 1] = (uint32_t)acc;  // two's complement top limb when negative
-  // + p where neg (the sum is then >= 0; the top limb wraps back to positive)
-  uint32_t c = 0;
-  const uint32_t msk = neg ? 0xffffffffu : 0u;
-#pragma unroll
-  for (int i = 0; i < N; i++) {
-    const uint32_t s = r.v[i] + (P::p(i) & msk) + c;
-    r.v[i] = i == N - 1 ? s : (s & LIMB_MASK);
-    c = s >> RADIX;
-  }
-  return r;
-}
-
 // Component of a * b (Fp2 = Fp[u]/(u^2 - BETA)), inputs < 4p per component,
 // result < 2p.
 template <class P, int BETA>
