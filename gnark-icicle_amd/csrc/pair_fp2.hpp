@@ -190,7 +190,7 @@ GM_DEV PairPt<P> pair_load_pt(const uint32_t* __restrict__ pt) {
 }
 
 #ifndef GM_PAIR_WPE
-#define GM_PAIR_WPE 1
+#define GM_PAIR_WPE 1  // no cap; per-TU override (msm_bls12377_g2.hip)
 #endif
 #define GM_PAIR_ATTR __attribute__((amdgpu_waves_per_eu(GM_PAIR_WPE)))
 template <class P, int BETA>
