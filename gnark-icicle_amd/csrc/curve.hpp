@@ -244,6 +244,47 @@ GM_DEV XYZZ<F> xyzz_add(const XYZZ<F>& a, const XYZZ<F>& b) {
   return r;
 }
 
+// canonical form of a point whose coordinates are < 2p
+template <class P>
+GM_DEV XYZZ<Fe<P>> xyzz_canon2(const XYZZ<Fe<P>>& a) {
+  return {fe_canon<1>(a.x), fe_canon<1>(a.y), fe_canon<1>(a.zz), fe_canon<1>(a.zzz)};
+}
+
+// Lazily reduced a + b (G1 bucket fixup and reduction): coordinates < 2p in and
+// out (canonical values qualify).  Product inputs stay below 4p x 4p = 16 p^2.
+// A lazily reduced zz is a non-zero residue unless the point is infinity (set
+// canonically), so fe_is_zero(zz) still tests infinity.
+template <class P>
+GM_DEV XYZZ<Fe<P>> xyzz_add_lz(const XYZZ<Fe<P>>& a, const XYZZ<Fe<P>>& b) {
+  using F = Fe<P>;
+  if (xyzz_is_inf(a)) return b;
+  if (xyzz_is_inf(b)) return a;
+  const F U1 = fe_mul_lz(a.x, b.zz);  // < 2p
+  const F U2 = fe_mul_lz(b.x, a.zz);
+  const F S1 = fe_mul_lz(a.y, b.zzz);
+  const F S2 = fe_mul_lz(b.y, a.zzz);
+  const F Pd = fe_sub_lz<2>(U2, U1);  // < 4p
+  const F R = fe_sub_lz<2>(S2, S1);   // < 4p
+  if (fe_is_zero_lz<4>(Pd)) {
+    if (fe_is_zero_lz<4>(R)) return xyzz_dbl(xyzz_canon2(a));
+    return xyzz_inf<F>();
+  }
+  const F PP = fe_sqr_lz(Pd);  // < 2p
+  const F PPP = fe_mul_lz(Pd, PP);
+  const F Q = fe_mul_lz(U1, PP);
+  F X3 = fe_sub_lz<4>(fe_sub_lz<2>(fe_sqr_lz(R), PPP), fe_add_lz(Q, Q));  // < 8p
+  fe_to2p<8>(X3);
+  // R (< 4p) (Q - X3 + 2p < 4p) - S1 PPP (< 4 p^2 < R' p), one reduction: < 2.1p
+  F Y3 = fe_mul2_redc(R, fe_sub_lz<2>(Q, X3), S1, PPP, true);
+  fe_to2p<4>(Y3);
+  XYZZ<F> r;
+  r.x = X3;
+  r.y = Y3;
+  r.zz = fe_mul_lz(fe_mul_lz(a.zz, b.zz), PP);
+  r.zzz = fe_mul_lz(fe_mul_lz(a.zzz, b.zzz), PPP);
+  return r;
+}
+
 // Affine point in gnark layout (X then Y, each Coord<F>::WORDS u32) -> internal.
 template <class F>
 GM_DEV Affine<F> load_affine_gnark(const uint32_t* __restrict__ src) {

@@ -335,6 +335,19 @@ inline bool g2_pairs() {
   return on;
 }
 
+// Full adds of the fixup / reduction kernels: lazily reduced for G1
+// (xyzz_add_lz, canonical on store), canonical xyzz_add otherwise.
+template <class F>
+struct FullAdd {
+  GM_DEV static XYZZ<F> add(const XYZZ<F>& a, const XYZZ<F>& b) { return xyzz_add(a, b); }
+  GM_DEV static XYZZ<F> canon(const XYZZ<F>& a) { return a; }
+};
+template <class P>
+struct FullAdd<Fe<P>> {
+  GM_DEV static XYZZ<Fe<P>> add(const XYZZ<Fe<P>>& a, const XYZZ<Fe<P>>& b) { return xyzz_add_lz(a, b); }
+  GM_DEV static XYZZ<Fe<P>> canon(const XYZZ<Fe<P>>& a) { return xyzz_canon2(a); }
+};
+
 // Merge the partial sums of buckets cut by slice edges.  Bucket b spans slices
 // t0..t1 and its sum is part_last[t0] + part_first[t0+1] + ... + part_first[t1].
 // Spans up to FIX_SERIAL slices are summed by one thread; longer spans (a huge
@@ -360,8 +373,8 @@ __global__ void __launch_bounds__(128) k_msm_fixup(const uint32_t* __restrict__ 
     return;
   }
   XYZZ<F> acc = part_last[t0];
-  for (uint32_t t = t0 + 1; t <= t1; t++) acc = xyzz_add(acc, part_first[t]);
-  buckets[b] = acc;
+  for (uint32_t t = t0 + 1; t <= t1; t++) acc = FullAdd<F>::add(acc, part_first[t]);
+  buckets[b] = FullAdd<F>::canon(acc);
 }
 
 // One level d of the pairwise tree over part_first[t0+1 .. t1] of every long span.
@@ -377,7 +390,7 @@ __global__ void __launch_bounds__(128) k_msm_fix_tree(const uint32_t* __restrict
   if (t1 - t0 <= FIX_SERIAL || t <= t0) return;
   const uint32_t rel = t - (t0 + 1), len = t1 - t0, step = 1u << d;
   if ((rel & ((step << 1) - 1)) == 0 && rel + step < len)
-    part_first[t] = xyzz_add(part_first[t], part_first[t + step]);
+    part_first[t] = FullAdd<F>::canon(FullAdd<F>::add(part_first[t], part_first[t + step]));
 }
 
 template <class F>
@@ -391,7 +404,7 @@ __global__ void __launch_bounds__(128) k_msm_fixup_long(const uint32_t* __restri
   if (be == bs) return;
   const uint32_t t0 = bs / K, t1 = (be - 1) / K;
   if (t1 - t0 <= FIX_SERIAL) return;
-  buckets[b] = xyzz_add(part_last[t0], part_first[t0 + 1]);
+  buckets[b] = FullAdd<F>::canon(FullAdd<F>::add(part_last[t0], part_first[t0 + 1]));
 }
 
 // ---------------------------------------------------------------------------
@@ -427,11 +440,11 @@ __global__ void __launch_bounds__(128) k_msm_seg(const XYZZ<F>* __restrict__ buc
   const XYZZ<F>* B = buckets + (size_t)w * nb + (size_t)s * L;
   XYZZ<F> S = B[L - 1], T = S;
   for (int j = (int)L - 2; j >= 0; j--) {
-    S = xyzz_add(S, B[j]);
-    T = xyzz_add(T, S);
+    S = FullAdd<F>::add(S, B[j]);
+    T = FullAdd<F>::add(T, S);
   }
-  nodes[2 * (size_t)t] = S;
-  nodes[2 * (size_t)t + 1] = T;
+  nodes[2 * (size_t)t] = FullAdd<F>::canon(S);
+  nodes[2 * (size_t)t + 1] = FullAdd<F>::canon(T);
 }
 
 // One tree level group: block (w, j) merges nodes [j*NT, (j+1)*NT) of window w
@@ -457,7 +470,7 @@ __global__ void __launch_bounds__(BS_THREADS) k_msm_bitsum(const XYZZ<F>* __rest
       const uint32_t t = threadIdx.x;
       if (t < tasks) {
         const uint32_t p = t / qc, q = t % qc, base = p * 2 * child;
-        r0 = (q + 1 < qc) ? xyzz_add(X[base + q], X[base + child + q]) : X[base + child];
+        r0 = (q + 1 < qc) ? FullAdd<F>::canon(FullAdd<F>::add(X[base + q], X[base + child + q])) : X[base + child];
         s0 = base + q;
       }
     }
@@ -465,7 +478,7 @@ __global__ void __launch_bounds__(BS_THREADS) k_msm_bitsum(const XYZZ<F>* __rest
       const uint32_t t = threadIdx.x + blockDim.x;
       if (t < tasks) {
         const uint32_t p = t / qc, q = t % qc, base = p * 2 * child;
-        r1 = (q + 1 < qc) ? xyzz_add(X[base + q], X[base + child + q]) : X[base + child];
+        r1 = (q + 1 < qc) ? FullAdd<F>::canon(FullAdd<F>::add(X[base + q], X[base + child + q])) : X[base + child];
         s1 = base + q;
       }
     }
