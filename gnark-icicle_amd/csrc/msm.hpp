@@ -2,6 +2,7 @@
 #pragma once
 #include <cstddef>
 #include <cstdint>
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 #include "curves.hpp"
 
@@ -51,13 +52,23 @@ struct MsmPlan {
   uint32_t Wred = 0;  // windows reduced separately: W (plain) or 1 (shared buckets)
   size_t n = 0, M = 0;  // M: upper bound on the sorted entries (n * W); offsets[total] = actual
   size_t npts = 0;    // points addressable through the plan (bounds check)
+  int bits = 0;       // scalar bits the digits cover (FR_BITS; 127 for a GLV split)
   uint32_t* keys = nullptr;     // sorted bucket keys (window-major bucket index), offsets[total] entries
   uint32_t* vals = nullptr;     // point index | sign << 31
   uint32_t* offsets = nullptr;  // total + 1 bucket start offsets
 };
+// glv (BN254 plain layout only): each scalar k is split k = k1 + k2 lambda with
+// |k1|, |k2| < 2^127, over 2n points [P_0..P_{n-1}, phi(P_0)..phi(P_{n-1})]
+// (msm_device_launch builds them): half the windows, so half the buckets to
+// reduce, for the same number of bucket adds.
 template <class C>
 int msm_plan(gm_ctx* ctx, Arena& arena, const void* scalars_dev, size_t n, const MsmPrecomp* pre,
-             MsmPlan& plan);
+             MsmPlan& plan, bool glv = false);
+// GLV used for plain BN254 G1 MSMs from gnark-layout points (GM_MSM_GLV=0 disables)
+inline bool msm_glv_enabled() {
+  static const bool on = !(getenv("GM_MSM_GLV") && getenv("GM_MSM_GLV")[0] == '0');
+  return on;
+}
 template <class C, bool G2>
 int msm_run(gm_ctx* ctx, const MsmPlan& plan, const void* points_internal,
             typename GroupSel<C, G2>::HF (&jac_out)[3]);

@@ -31,6 +31,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 namespace gm {
 
@@ -115,6 +116,141 @@ __global__ void __launch_bounds__(1024) k_msm_digits(const uint32_t* __restrict_
   __syncthreads();
   for (uint32_t q = t; q < NC; q += DG_THREADS)
     if (dg_lds[q]) atomicAdd(&ccount[q], dg_lds[q]);
+}
+
+// ---------------------------------------------------------------------------
+// GLV split for BN254 G1: phi(x, y) = (beta x, y) = [lambda] P with beta, lambda
+// primitive cube roots of unity (p resp. r).  Short lattice basis of
+// {(a, b) : a + b lambda = 0 mod r}: v1 = (a1, b1), v2 = (a2, b2) with
+// a1 = b2 - |b1| ~ 2^126.8, b1 = -a2, a2 ~ 2^63.1.  c1 = floor(k g1 / 2^384),
+// c2 = floor(k g2 / 2^384) with g1 = floor(2^384 b2 / r), g2 = floor(2^384 |b1| / r)
+// undershoot b2 k / r and |b1| k / r by e1, e2 in [0, 1 + 2^-130), so
+// k1 = k - c1 a1 - c2 a2 = e1 a1 + e2 a2 lies in [0, 2^127) and
+// k2 = c1 |b1| - c2 b2 = -(e1 |b1|) + e2 b2 in (-2^127, 2^127): both are exact
+// in 128-bit wrap-around arithmetic.  Constants derived by
+// tools/glv_constants.py (checked there against the oracle's group law).
+// ---------------------------------------------------------------------------
+struct GlvBn254 {
+  GM_HD static constexpr uint64_t g1(int i) {
+    constexpr uint64_t a[5] = {0x163b4843cb4b9a5eull, 0x149d540fd5e495ccull, 0x5398fd0300ff6565ull,
+                               0x4ccef014a773d2d2ull, 0x0000000000000002ull};
+    return a[i];
+  }
+  GM_HD static constexpr uint64_t g2(int i) {
+    constexpr uint64_t a[4] = {0x8fa7d32d2fafba64ull, 0x6eb9c714773a6ef2ull, 0xd91d232ec7e0b3d7ull,
+                               0x0000000000000002ull};
+    return a[i];
+  }
+  static constexpr uint64_t A1_LO = 0x8211bbeb7d4f1128ull, A1_HI = 0x6f4d8248eeb859fcull;
+  static constexpr uint64_t A2 = 0x89d3256894d213e3ull;  // = |b1|
+  static constexpr uint64_t B2_LO = 0x0be4e1541221250bull, B2_HI = 0x6f4d8248eeb859fdull;
+  // beta in the internal radix-2^29 Montgomery form (beta * 2^261 mod p)
+  GM_HD static constexpr uint32_t beta29(int i) {
+    constexpr uint32_t a[9] = {0x18ccb791u, 0x175b1c3au, 0x0b83d6e2u, 0x0e8ed071u, 0x1282bee2u,
+                               0x04220e84u, 0x1fe4017fu, 0x15084d4au, 0x00169119u};
+    return a[i];
+  }
+};
+
+// floor(k * G / 2^384) for a 256-bit k and a G of NG 64-bit limbs (< 2^128 here)
+template <int NG, class GF>
+GM_DEV unsigned __int128 glv_mulshift(const uint64_t (&k)[4], GF g) {
+  uint64_t t[4 + NG] = {};
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    uint64_t carry = 0;
+#pragma unroll
+    for (int j = 0; j < NG; j++) {
+      const unsigned __int128 v = (unsigned __int128)k[i] * g(j) + t[i + j] + carry;
+      t[i + j] = (uint64_t)v;
+      carry = (uint64_t)(v >> 64);
+    }
+    t[i + NG] = carry;
+  }
+  return ((unsigned __int128)t[7] << 64) | t[6];
+}
+
+// one scalar's signed digits, written at dig[w * g.n + i]; flip: negate them
+template <class Fr>
+GM_DEV void emit_digits(const FeG<Fr>& k, uint32_t flip, uint32_t i, const DigitGeom& g, uint32_t* __restrict__ dig,
+                        uint32_t* lds) {
+  const uint32_t mask = (1u << g.c) - 1;
+  uint32_t carry = 0;
+  for (uint32_t w = 0; w < g.W; w++) {
+    const uint32_t raw = window_bits(k, w * g.c, mask) + carry;
+    uint32_t d, neg;
+    if (raw > g.nb) {
+      d = (1u << g.c) - raw;
+      carry = 1;
+      neg = 1;
+    } else {
+      d = raw;
+      carry = 0;
+      neg = 0;
+    }
+    dig[(size_t)w * g.n + i] = d ? (d - 1) | ((neg ^ flip) << 31) : 0xffffffffu;
+    if (d) atomicAdd(&lds[(w * g.nb + d - 1) >> g.F], 1u);
+  }
+}
+
+// k_msm_digits for the GLV split (plain layout): thread i writes the digits of
+// k1 at virtual point i and of k2 at virtual point n0 + i (g.n = 2 n0).
+template <int Unused = 0>
+__global__ void __launch_bounds__(1024) k_msm_digits_glv(const uint32_t* __restrict__ scalars, DigitGeom g,
+                                                         uint32_t n0, uint32_t NC, uint32_t* __restrict__ dig,
+                                                         uint32_t* __restrict__ ccount) {
+  extern __shared__ uint32_t dg_lds[];
+  const uint32_t t = threadIdx.x;
+  for (uint32_t q = t; q < NC; q += DG_THREADS) dg_lds[q] = 0;
+  __syncthreads();
+  const uint32_t base = blockIdx.x * DG_THREADS * DG_PPT;
+  for (uint32_t r = 0; r < DG_PPT; r++) {
+    const uint32_t i = base + r * DG_THREADS + t;
+    if (i >= n0) break;
+    const FeG<Bn254Fr> k = load_scalar_canonical<Bn254Fr>(scalars, i);
+    uint64_t k64[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) k64[j] = (uint64_t)k.w[2 * j] | ((uint64_t)k.w[2 * j + 1] << 32);
+    using U = unsigned __int128;
+    const U c1 = glv_mulshift<5>(k64, GlvBn254::g1);
+    const U c2 = glv_mulshift<4>(k64, GlvBn254::g2);
+    const U a1 = ((U)GlvBn254::A1_HI << 64) | GlvBn254::A1_LO;
+    const U b2 = ((U)GlvBn254::B2_HI << 64) | GlvBn254::B2_LO;
+    const U klo = ((U)k64[1] << 64) | k64[0];
+    const U k1 = klo - c1 * a1 - c2 * (U)GlvBn254::A2;  // in [0, 2^127)
+    U k2 = c1 * (U)GlvBn254::A2 - c2 * b2;               // signed, |k2| < 2^127
+    const uint32_t neg2 = (uint32_t)(k2 >> 127);
+    if (neg2) k2 = (U)0 - k2;
+    FeG<Bn254Fr> m1, m2;
+#pragma unroll
+    for (int j = 0; j < Bn254Fr::NG; j++) {
+      m1.w[j] = j < 4 ? (uint32_t)(k1 >> (32 * j)) : 0u;
+      m2.w[j] = j < 4 ? (uint32_t)(k2 >> (32 * j)) : 0u;
+    }
+    emit_digits<Bn254Fr>(m1, 0u, i, g, dig, dg_lds);
+    emit_digits<Bn254Fr>(m2, neg2, n0 + i, g, dig, dg_lds);
+  }
+  __syncthreads();
+  for (uint32_t q = t; q < NC; q += DG_THREADS)
+    if (dg_lds[q]) atomicAdd(&ccount[q], dg_lds[q]);
+}
+
+// gnark-layout BN254 G1 points -> internal layout, plus phi(P_i) = (beta x, y)
+// at n + i (the GLV point set)
+template <int Unused = 0>
+__global__ void __launch_bounds__(256) k_msm_convert_points_glv(const uint32_t* __restrict__ src, size_t n,
+                                                                uint32_t* __restrict__ dst) {
+  using F = Fe<Bn254Fp>;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  constexpr int PW = 2 * Coord<F>::WORDS;
+  Affine<F> a = load_affine_gnark<F>(src + i * PW);
+  store_affine_packed<F>(dst + i * PW, a);
+  F beta;
+#pragma unroll
+  for (int j = 0; j < F::N; j++) beta.v[j] = GlvBn254::beta29(j);
+  a.x = fe_mul(a.x, beta);
+  store_affine_packed<F>(dst + (n + i) * PW, a);
 }
 
 // ---------------------------------------------------------------------------
@@ -530,11 +666,22 @@ static int choose_window(size_t n, int bits) {
 // Keys, sort and bucket offsets for one scalar vector (see MsmPlan).
 template <class C>
 int msm_plan(gm_ctx* ctx, Arena& arena, const void* scalars_dev, size_t n, const MsmPrecomp* pre,
-             MsmPlan& plan) {
+             MsmPlan& plan, bool glv) {
   hipStream_t st = ctx->stream;
   plan = MsmPlan();
   plan.n = n;
+  plan.bits = C::FR_BITS;
   if (n == 0) return GM_OK;
+  if (glv && (!std::is_same<typename C::Fr, Bn254Fr>::value || (pre && pre->c))) {
+    set_error("msm: the GLV split is BN254 plain-layout only");
+    return GM_ERR_INVALID;
+  }
+  const size_t n0 = n;  // scalars
+  if (glv) {            // virtual points: P_i and phi(P_i)
+    n = 2 * n0;
+    plan.n = n;
+    plan.bits = 127;
+  }
   if (n >= (size_t(1) << 31)) {
     set_error("msm: n must be < 2^31");
     return GM_ERR_INVALID;
@@ -547,9 +694,9 @@ int msm_plan(gm_ctx* ctx, Arena& arena, const void* scalars_dev, size_t n, const
   }
   const uint32_t c = shared ? pre->c
                             : (ctx->msm_c_override ? (uint32_t)ctx->msm_c_override
-                                                   : (uint32_t)choose_window(n, C::FR_BITS));
+                                                   : (uint32_t)choose_window(n, plan.bits));
   // ceil((bits+1)/c): the top signed digit never carries
-  const uint32_t W = shared ? pre->W : (C::FR_BITS + 1 + c - 1) / c;
+  const uint32_t W = shared ? pre->W : (uint32_t)(plan.bits + 1 + c - 1) / c;
   plan.c = c;
   plan.W = W;
   plan.nb = 1u << (c - 1);
@@ -572,7 +719,11 @@ int msm_plan(gm_ctx* ctx, Arena& arena, const void* scalars_dev, size_t n, const
   sg.T = plan.total;
   sg.M = M;
   sg.F = 4;
-  while (sg.F < 13 && (double)M * std::ldexp(1.0, (int)sg.F + 1) <= 2048.0 * sg.T) sg.F++;
+  // A GLV plan's windows are full width (|k1|, |k2| < 0.87 * 2^127: no narrow top
+  // window) with twice the entries per bucket: ~4K-entry bins keep one pass-1
+  // block within 512 bins (no middle pass) and still fit S2_STAGE.
+  const double bin_entries = glv ? 4096.0 : 2048.0;
+  while (sg.F < 13 && (double)M * std::ldexp(1.0, (int)sg.F + 1) <= bin_entries * sg.T) sg.F++;
   auto bins = [&](uint32_t sh) { return (uint32_t)(((uint64_t)sg.T + (1ull << sh) - 1) >> sh); };
   auto touched = [&](uint32_t sh) { return shared ? bins(sh) : std::max(1u, plan.nb >> sh); };
   // GM_MSM_SORT_MING: minimum G (tests exercise the middle pass at small sizes)
@@ -607,9 +758,16 @@ int msm_plan(gm_ctx* ctx, Arena& arena, const void* scalars_dev, size_t n, const
   {
     ProfScope ps(ctx, "msm_digits");
     GM_HIP(hipMemsetAsync(scount.p, 0, sizeof(uint32_t) * sg.NS, st));
-    hipLaunchKernelGGL(k_msm_digits<typename C::Fr>, dim3(blocks_for(n, DG_THREADS * DG_PPT)), dim3(DG_THREADS),
-                       sizeof(uint32_t) * sg.NS, st, reinterpret_cast<const uint32_t*>(scalars_dev), g, sg.NS,
-                       dig.as<uint32_t>(), scount.as<uint32_t>());
+    if constexpr (std::is_same<typename C::Fr, Bn254Fr>::value) {
+      if (glv)
+        hipLaunchKernelGGL(k_msm_digits_glv<0>, dim3(blocks_for(n0, DG_THREADS * DG_PPT)), dim3(DG_THREADS),
+                         sizeof(uint32_t) * sg.NS, st, reinterpret_cast<const uint32_t*>(scalars_dev), g,
+                           (uint32_t)n0, sg.NS, dig.as<uint32_t>(), scount.as<uint32_t>());
+    }
+    if (!glv)
+      hipLaunchKernelGGL(k_msm_digits<typename C::Fr>, dim3(blocks_for(n, DG_THREADS * DG_PPT)), dim3(DG_THREADS),
+                         sizeof(uint32_t) * sg.NS, st, reinterpret_cast<const uint32_t*>(scalars_dev), g, sg.NS,
+                         dig.as<uint32_t>(), scount.as<uint32_t>());
     GM_HIP(hipGetLastError());
   }
   {
@@ -821,7 +979,7 @@ int msm_launch(gm_ctx* ctx, Arena& arena, const MsmPlan& plan, const void* point
   // shared).  Large MSMs whose top window is narrow (2^24: 1024-4096 entries per
   // top digit) sync on the max span first.
   {
-    const int top_bits = C::FR_BITS - (int)(t.c * (t.W - 1));
+    const int top_bits = plan.bits - (int)(t.c * (t.W - 1));
     double fullest = (double)plan.n / std::ldexp(1.0, top_bits > 0 ? top_bits : 0);
     if (t.Wr == 1 && t.W > 1) fullest += (double)(t.W - 1) * (double)plan.n / (double)t.nb;
     if (fullest > 0.5 * FIX_SERIAL * t.K) {
@@ -916,19 +1074,27 @@ int msm_device_launch(gm_ctx* ctx, Arena& arena, const void* scalars_dev, const 
   int rc;
   const void* pts = points_dev;
   DevBuf ipts;
+  bool glv = false;
   if (!points_internal && n) {
     if (pre && pre->c) {
       set_error("msm: a precomputed point set must be device-internal");
       return GM_ERR_INVALID;
     }
-    if ((rc = ipts.alloc(arena, 2 * Coord<DF>::WORDS * sizeof(uint32_t) * n))) return rc;
+    glv = !G2 && std::is_same<typename C::Fr, Bn254Fr>::value && msm_glv_enabled();
+    if ((rc = ipts.alloc(arena, 2 * Coord<DF>::WORDS * sizeof(uint32_t) * n * (glv ? 2 : 1)))) return rc;
     ProfScope ps(ctx, "msm_convert_points");
-    hipLaunchKernelGGL(k_msm_convert_points<DF>, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream,
-                       reinterpret_cast<const uint32_t*>(points_dev), n, ipts.as<uint32_t>());
+    if constexpr (!G2 && std::is_same<typename C::Fr, Bn254Fr>::value) {
+      if (glv)
+        hipLaunchKernelGGL(k_msm_convert_points_glv<0>, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream,
+                           reinterpret_cast<const uint32_t*>(points_dev), n, ipts.as<uint32_t>());
+    }
+    if (!glv)
+      hipLaunchKernelGGL(k_msm_convert_points<DF>, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream,
+                         reinterpret_cast<const uint32_t*>(points_dev), n, ipts.as<uint32_t>());
     pts = ipts.p;
   }
   MsmPlan plan;
-  if ((rc = msm_plan<C>(ctx, arena, scalars_dev, n, pre, plan))) return rc;
+  if ((rc = msm_plan<C>(ctx, arena, scalars_dev, n, pre, plan, glv))) return rc;
   return msm_launch<C, G2>(ctx, arena, plan, pts, t);
 }
 
@@ -988,6 +1154,6 @@ int msm_precompute_points(gm_ctx* ctx, const void* gnark_points, size_t n, const
   template int msm_device<C, G2>(gm_ctx*, const void*, const void*, size_t,                    \
                                  typename GroupSel<C, G2>::HF (&)[3], bool, const MsmPrecomp*);
 #define GM_MSM_INSTANTIATE_PLAN(C) \
-  template int msm_plan<C>(gm_ctx*, Arena&, const void*, size_t, const MsmPrecomp*, MsmPlan&);
+  template int msm_plan<C>(gm_ctx*, Arena&, const void*, size_t, const MsmPrecomp*, MsmPlan&, bool);
 
 }  // namespace gm

@@ -432,3 +432,40 @@ def test_msm_async_pipelined(gm_ctx, oracle):
         for c in cases:
             c[3].free()
             c[4].free()
+
+
+@pytest.mark.parametrize("window", [0, 11, 16])
+def test_msm_glv_split_boundaries(gm_ctx, oracle, window):
+    """BN254 G1 MSMs from gnark-layout points run the GLV split (k = k1 + k2 lambda,
+    |k1|, |k2| < 2^127, points P_i and phi(P_i) = (beta x, y); msm_impl.hpp
+    GlvBn254): scalars at the split's edges -- lambda, r - lambda, the basis
+    entries, k2 of both signs, r - 1 -- plus random ones, against the oracle's
+    unsplit Pippenger."""
+    c = pyref.BN254
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "glv_constants", os.path.join(os.path.dirname(__file__), "..", "tools", "glv_constants.py"))
+    glv = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(glv)
+    d = glv.derive()
+    r, lam = c.r, d["lam"]
+    special = [0, 1, 2, r - 1, r - 2, lam, r - lam, lam + 1, lam - 1, d["a1"], d["b2"], r - d["b2"],
+               d["a2"], r - d["a2"], (r - 1) // 2, (r + 1) // 2, 1 << 253, (1 << 127) - 1, 1 << 127]
+    n = 4096 + 19
+    sc = pyref.random_scalars(c, n, 0x61F)
+    sc[:len(special)] = special
+    sb = b"".join(pyref.encode_fr(c, s) for s in sc)
+    pb = _random_points_host(gm_ctx, "bn254", False, n, 0x620)
+    pb = pyref.encode_point(c, None, False) + pb[64:]  # an infinity point
+    S = gm_ctx.copy_to_device(sb)
+    P = gm_ctx.copy_to_device(pb)
+    exp = oracle.msm("bn254", False, sb, pb)
+    try:
+        gm_ctx.set_msm_window(window)
+        for m in (1, 7, 64, n):
+            exp_m = exp if m == n else oracle.msm("bn254", False, sb[:32 * m], pb[:64 * m])
+            assert gm_ctx.msm("bn254", S, P, m)[1] == exp_m, (window, m)
+    finally:
+        gm_ctx.set_msm_window(0)
+        S.free()
+        P.free()
