@@ -156,9 +156,11 @@ def main():
     acc_avg_ms = acc_ms / max(acc_cnt, 1)
     alg_bytes = MSM_BYTES_PER_POINT * n  # per launch: one MSM of n points
     achieved_gbs = alg_bytes / (acc_avg_ms * 1e-3) / 1e9 if acc_avg_ms > 0 else 0.0
-    c = max(8, min(20, n.bit_length() - 1 - 4))   # gm choose_window
-    windows = -(-255 // c)                          # ceil((254 + 1) / c)
-    mads = n * windows * MADS_PER_MIXED_ADD         # ~one XYZZ mixed add per (point, window)
+    glv = os.environ.get("GM_MSM_GLV", "1")[:1] != "0"  # BN254 GLV split (msm_impl.hpp GlvBn254)
+    npts = 2 * n if glv else n                      # virtual points: P_i and phi(P_i)
+    c = max(8, min(20, npts.bit_length() - 1 - 4))  # gm choose_window
+    windows = -(-128 // c) if glv else -(-255 // c)  # ceil((bits + 1) / c), bits = 127 / 254
+    mads = npts * windows * MADS_PER_MIXED_ADD      # ~one XYZZ mixed add per (point, window)
     tmads = mads / (acc_avg_ms * 1e-3) / 1e12 if acc_avg_ms > 0 else 0.0
     roofline = {
         "kernel": "k_msm_accum_seg<Fe<Bn254Fp>> (msm_accum_g1)",
@@ -172,11 +174,12 @@ def main():
         "bytes_per_launch": alg_bytes,
         "int_alu": {"achieved": round(tmads, 3), "peak": round(MAD_PEAK_T, 2), "unit": "T v_mad_u64_u32/s",
                     "frac": round(tmads / MAD_PEAK_T, 4),
-                    "work": "%d points x %d windows XYZZ mixed adds x %d mads" % (n, windows, MADS_PER_MIXED_ADD)},
+                    "work": "%d %spoints x %d windows XYZZ mixed adds x %d mads" % (
+                        npts, "GLV (P, phi(P)) " if glv else "", windows, MADS_PER_MIXED_ADD)},
         "valu": load_pmc_valu("k_msm_accum_seg<Fe<Bn254Fp> >"),
         "note": "bound=hbm is the bench contract's roofline for this non-MFMA path; the kernel is NOT HBM-bound: "
                 "its binding resource is VALU issue -- rocprofv3 PMC (profiles/r02_pmc_valu.json) shows VALUBusy "
-                "~0.88 (gfx9 formula, 4 cycles/instr) for k_msm_accum_seg, ~2880 VALU instructions per mixed add; "
+                "~0.89 (gfx9 formula, 4 cycles/instr) for k_msm_accum_seg, ~2750 VALU instructions per mixed add; "
                 "int_alu prices the v_mad_u64_u32 work at the measured mad-only issue peak (DESIGN.md section 3)",
     }
     kernel_ms = {k: round(v[0] / max(v[1], 1), 4) for k, v in stats.items()}
