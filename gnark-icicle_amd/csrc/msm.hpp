@@ -69,6 +69,11 @@ inline bool msm_glv_enabled() {
   static const bool on = !(getenv("GM_MSM_GLV") && getenv("GM_MSM_GLV")[0] == '0');
   return on;
 }
+// ... and for BN254 G2 (phi(x, y) = (beta^2 x, y) on the twist; GM_MSM_GLV_G2=0 disables)
+inline bool msm_glv_g2_enabled() {
+  static const bool on = !(getenv("GM_MSM_GLV_G2") && getenv("GM_MSM_GLV_G2")[0] == '0');
+  return on;
+}
 template <class C, bool G2>
 int msm_run(gm_ctx* ctx, const MsmPlan& plan, const void* points_internal,
             typename GroupSel<C, G2>::HF (&jac_out)[3]);

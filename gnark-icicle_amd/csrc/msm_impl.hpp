@@ -150,7 +150,29 @@ struct GlvBn254 {
                                0x04220e84u, 0x1fe4017fu, 0x15084d4au, 0x00169119u};
     return a[i];
   }
+  // G2 (the twist y^2 = x^3 + b' over Fp2): (x, y) -> (beta^2 x, y) is [lambda] on
+  // the r-torsion (the other cube root of unity of Fp; tools/glv_constants.py)
+  GM_HD static constexpr uint32_t beta29_g2(int i) {
+    constexpr uint32_t a[9] = {0x0a337995u, 0x158d1d23u, 0x189c9b98u, 0x12fa4e45u, 0x185faadcu,
+                               0x0176f16du, 0x0eed93bau, 0x14291140u, 0x000c0afeu};
+    return a[i];
+  }
 };
+
+// x -> beta x of the GLV endomorphism, G1 (Fp) and G2 (Fp2, beta in Fp)
+GM_DEV Fe<Bn254Fp> glv_phi_x(const Fe<Bn254Fp>& x) {
+  Fe<Bn254Fp> b;
+#pragma unroll
+  for (int j = 0; j < Bn254Fp::N; j++) b.v[j] = GlvBn254::beta29(j);
+  return fe_mul(x, b);
+}
+template <int B>
+GM_DEV Fe2<Bn254Fp, B> glv_phi_x(const Fe2<Bn254Fp, B>& x) {
+  Fe<Bn254Fp> b;
+#pragma unroll
+  for (int j = 0; j < Bn254Fp::N; j++) b.v[j] = GlvBn254::beta29_g2(j);
+  return {fe_mul(x.a0, b), fe_mul(x.a1, b)};
+}
 
 // floor(k * G / 2^384) for a 256-bit k and a G of NG 64-bit limbs (< 2^128 here)
 template <int NG, class GF>
@@ -237,19 +259,15 @@ __global__ void __launch_bounds__(1024) k_msm_digits_glv(const uint32_t* __restr
 
 // gnark-layout BN254 G1 points -> internal layout, plus phi(P_i) = (beta x, y)
 // at n + i (the GLV point set)
-template <int Unused = 0>
+template <class F>
 __global__ void __launch_bounds__(256) k_msm_convert_points_glv(const uint32_t* __restrict__ src, size_t n,
                                                                 uint32_t* __restrict__ dst) {
-  using F = Fe<Bn254Fp>;
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   constexpr int PW = 2 * Coord<F>::WORDS;
   Affine<F> a = load_affine_gnark<F>(src + i * PW);
   store_affine_packed<F>(dst + i * PW, a);
-  F beta;
-#pragma unroll
-  for (int j = 0; j < F::N; j++) beta.v[j] = GlvBn254::beta29(j);
-  a.x = fe_mul(a.x, beta);
+  a.x = glv_phi_x(a.x);
   store_affine_packed<F>(dst + (n + i) * PW, a);
 }
 
@@ -1080,12 +1098,12 @@ int msm_device_launch(gm_ctx* ctx, Arena& arena, const void* scalars_dev, const 
       set_error("msm: a precomputed point set must be device-internal");
       return GM_ERR_INVALID;
     }
-    glv = !G2 && std::is_same<typename C::Fr, Bn254Fr>::value && msm_glv_enabled();
+    glv = std::is_same<typename C::Fr, Bn254Fr>::value && msm_glv_enabled() && (!G2 || msm_glv_g2_enabled());
     if ((rc = ipts.alloc(arena, 2 * Coord<DF>::WORDS * sizeof(uint32_t) * n * (glv ? 2 : 1)))) return rc;
     ProfScope ps(ctx, "msm_convert_points");
-    if constexpr (!G2 && std::is_same<typename C::Fr, Bn254Fr>::value) {
+    if constexpr (std::is_same<typename C::Fr, Bn254Fr>::value) {
       if (glv)
-        hipLaunchKernelGGL(k_msm_convert_points_glv<0>, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream,
+        hipLaunchKernelGGL(k_msm_convert_points_glv<DF>, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream,
                            reinterpret_cast<const uint32_t*>(points_dev), n, ipts.as<uint32_t>());
     }
     if (!glv)

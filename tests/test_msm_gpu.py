@@ -434,13 +434,13 @@ def test_msm_async_pipelined(gm_ctx, oracle):
             c[4].free()
 
 
-@pytest.mark.parametrize("window", [0, 11, 16])
-def test_msm_glv_split_boundaries(gm_ctx, oracle, window):
-    """BN254 G1 MSMs from gnark-layout points run the GLV split (k = k1 + k2 lambda,
-    |k1|, |k2| < 2^127, points P_i and phi(P_i) = (beta x, y); msm_impl.hpp
-    GlvBn254): scalars at the split's edges -- lambda, r - lambda, the basis
-    entries, k2 of both signs, r - 1 -- plus random ones, against the oracle's
-    unsplit Pippenger."""
+@pytest.mark.parametrize("g2,window", [(False, 0), (False, 11), (False, 16), (True, 0), (True, 16)])
+def test_msm_glv_split_boundaries(gm_ctx, oracle, g2, window):
+    """BN254 G1 / G2 MSMs from gnark-layout points run the GLV split (k = k1 + k2
+    lambda, |k1|, |k2| < 2^127, points P_i and phi(P_i) = (beta x, y), beta^2 on
+    the G2 twist; msm_impl.hpp GlvBn254): scalars at the split's edges -- lambda,
+    r - lambda, the basis entries, k2 of both signs, r - 1 -- plus random ones,
+    against the oracle's unsplit Pippenger."""
     c = pyref.BN254
     import importlib.util
     spec = importlib.util.spec_from_file_location(
@@ -451,20 +451,21 @@ def test_msm_glv_split_boundaries(gm_ctx, oracle, window):
     r, lam = c.r, d["lam"]
     special = [0, 1, 2, r - 1, r - 2, lam, r - lam, lam + 1, lam - 1, d["a1"], d["b2"], r - d["b2"],
                d["a2"], r - d["a2"], (r - 1) // 2, (r + 1) // 2, 1 << 253, (1 << 127) - 1, 1 << 127]
-    n = 4096 + 19
+    n = 4096 + 19 if not g2 else 1024 + 19
+    pbytes = 128 if g2 else 64
     sc = pyref.random_scalars(c, n, 0x61F)
     sc[:len(special)] = special
     sb = b"".join(pyref.encode_fr(c, s) for s in sc)
-    pb = _random_points_host(gm_ctx, "bn254", False, n, 0x620)
-    pb = pyref.encode_point(c, None, False) + pb[64:]  # an infinity point
+    pb = _random_points_host(gm_ctx, "bn254", g2, n, 0x620)
+    pb = pyref.encode_point(c, None, g2) + pb[pbytes:]  # an infinity point
     S = gm_ctx.copy_to_device(sb)
     P = gm_ctx.copy_to_device(pb)
-    exp = oracle.msm("bn254", False, sb, pb)
+    exp = oracle.msm("bn254", g2, sb, pb)
     try:
         gm_ctx.set_msm_window(window)
         for m in (1, 7, 64, n):
-            exp_m = exp if m == n else oracle.msm("bn254", False, sb[:32 * m], pb[:64 * m])
-            assert gm_ctx.msm("bn254", S, P, m)[1] == exp_m, (window, m)
+            exp_m = exp if m == n else oracle.msm("bn254", g2, sb[:32 * m], pb[:pbytes * m])
+            assert gm_ctx.msm("bn254", S, P, m, g2)[1] == exp_m, (g2, window, m)
     finally:
         gm_ctx.set_msm_window(0)
         S.free()
