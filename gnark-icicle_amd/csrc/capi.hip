@@ -304,6 +304,14 @@ int gm_msm(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const void* 
 
 }  // extern "C"
 
+// MsmTail's pinned readback buffer goes back to its context (msm.hpp)
+void gm::MsmTail::release_stage() {
+  if (stage_ctx) tail_pinned_release(stage_ctx, stage_idx);
+  stage_ctx = nullptr;
+  stage_idx = -1;
+  stage = nullptr;
+}
+
 struct gm_msm_pending {
   gm_ctx* ctx;
   int curve, g2;

@@ -90,9 +90,16 @@ struct MsmTail {
   void *buckets = nullptr, *pfirst = nullptr, *plast = nullptr, *nodes_a = nullptr, *nodes_b = nullptr;
   void *wsum = nullptr, *errw = nullptr;
   uint8_t* stage = nullptr;  // pinned readback: 16 B (error, max span) + the exported nodes
+  gm_ctx* stage_ctx = nullptr;  // owner of `stage` (tail_pinned_acquire), released by msm_finish
+  int stage_idx = -1;
   hipEvent_t done = nullptr;
+  void release_stage();  // runtime.hpp: returns `stage` to the context
+  MsmTail() = default;
+  MsmTail(const MsmTail&) = delete;
+  MsmTail& operator=(const MsmTail&) = delete;
   ~MsmTail() {
     if (done) hipEventDestroy(done);
+    release_stage();
   }
 };
 template <class C, bool G2>

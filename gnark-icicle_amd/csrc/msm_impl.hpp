@@ -887,7 +887,10 @@ int msm_readback(gm_ctx* ctx, MsmTail& t) {
   constexpr int WORDS = Coord<DF>::WORDS;
   hipStream_t st = ctx->stream;
   const size_t wbytes = sizeof(uint32_t) * 4 * WORDS * t.Wr * t.Q;
-  if (int r = tail_pinned_buf(ctx, 16 + wbytes, &t.stage)) return r;
+  if (!t.stage) {  // a re-readback (after a long-span fixup) reuses the tail's buffer
+    if (int r = tail_pinned_acquire(ctx, 16 + wbytes, &t.stage, &t.stage_idx)) return r;
+    t.stage_ctx = ctx;
+  }
   GM_HIP(hipMemcpyAsync(t.stage, t.errw, 16, hipMemcpyDeviceToHost, st));
   GM_HIP(hipMemcpyAsync(t.stage + 16, t.wsum, wbytes, hipMemcpyDeviceToHost, st));
   if (!t.done) GM_HIP(hipEventCreateWithFlags(&t.done, hipEventDisableTiming));
@@ -1002,11 +1005,14 @@ int msm_launch(gm_ctx* ctx, Arena& arena, const MsmPlan& plan, const void* point
     if (t.Wr == 1 && t.W > 1) fullest += (double)(t.W - 1) * (double)plan.n / (double)t.nb;
     if (fullest > 0.5 * FIX_SERIAL * t.K) {
       uint8_t* pb;
-      if ((rc = tail_pinned_buf(ctx, 16, &pb))) return rc;
-      GM_HIP(hipMemcpyAsync(pb, errw.p, 16, hipMemcpyDeviceToHost, st));
-      GM_HIP(hipStreamSynchronize(st));
+      int pbi;
+      if ((rc = tail_pinned_acquire(ctx, 16, &pb, &pbi))) return rc;
+      const hipError_t e1 = hipMemcpyAsync(pb, errw.p, 16, hipMemcpyDeviceToHost, st);
+      const hipError_t e2 = e1 == hipSuccess ? hipStreamSynchronize(st) : e1;
       uint32_t ms;
       memcpy(&ms, pb + 4, 4);
+      tail_pinned_release(ctx, pbi);
+      GM_HIP(e2);
       if (ms > FIX_SERIAL) {
         if ((rc = msm_fix_long<C, G2>(ctx, t, ms))) return rc;
         GM_HIP(hipMemsetAsync(errw.as<uint32_t>() + 1, 0, 4, st));  // long spans resolved
@@ -1050,6 +1056,7 @@ int msm_finish(gm_ctx* ctx, MsmTail& t, typename GroupSel<C, G2>::HF (&jac_out)[
   const uint32_t Wr = t.Wr, Q = t.Q, c = t.c;
   std::vector<HF> hw(4 * (size_t)Wr * Q);
   memcpy(hw.data(), t.stage + 16, sizeof(HF) * hw.size());
+  t.release_stage();  // the buffer may serve the next readback
   // Host Horner over bit positions: window w contributes U_w at 2^(c w) and
   // Y_{w,b} at 2^(c w + log2 L + b) (b < Q - 2 = log2(nseg), so every exponent
   // stays below c (w + 1)).  Shared buckets: one window, w = 0.

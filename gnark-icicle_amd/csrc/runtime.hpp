@@ -70,9 +70,12 @@ struct gm_ctx {
   gm::ArenaState arena;
   gm::ArenaState slots[2];
   bool slot_busy[2] = {false, false};
-  // pinned readback buffers of deferred MSM tails (rotating)
-  void* tail_pinned[4] = {nullptr, nullptr, nullptr, nullptr};
-  int tail_next = 0;
+  // pinned readback buffers of deferred MSM tails; a buffer stays busy from
+  // msm_readback until its MSM's msm_finish (or the tail's destruction), so
+  // synchronous MSMs issued while async ones are pending never reuse it
+  static constexpr int TAIL_BUFS = 8;
+  void* tail_pinned[TAIL_BUFS] = {};
+  bool tail_busy[TAIL_BUFS] = {};
   // one stream per slot (gm_msm_async): two independent MSMs in flight overlap
   // on the device -- one's sort / reduction (HBM / latency-bound) runs beside the
   // other's accumulation (VALU-bound).  Created on first use.
@@ -206,25 +209,35 @@ struct SlotArena {
   SlotArena& operator=(const SlotArena&) = delete;
 };
 
-// Pinned readback buffer of a deferred MSM tail (4 rotating 512 KiB buffers).
-inline int tail_pinned_buf(gm_ctx* ctx, size_t bytes, uint8_t** out) {
+// Pinned readback buffer of a deferred MSM tail: the first free one of the
+// context's TAIL_BUFS 512 KiB buffers, marked busy until tail_pinned_release.
+inline int tail_pinned_acquire(gm_ctx* ctx, size_t bytes, uint8_t** out, int* idx) {
   constexpr size_t CAP = size_t(512) << 10;
   if (bytes > CAP) {
     set_error("msm: readback larger than the tail buffer");
     return GM_ERR_INVALID;
   }
-  void*& b = ctx->tail_pinned[ctx->tail_next];
-  ctx->tail_next = (ctx->tail_next + 1) & 3;
-  if (!b) {
-    hipError_t e = hipHostMalloc(&b, CAP, hipHostMallocDefault);
-    if (e != hipSuccess) {
-      b = nullptr;
-      set_error(std::string("hipHostMalloc: ") + hipGetErrorString(e));
-      return GM_ERR_OOM;
+  for (int i = 0; i < gm_ctx::TAIL_BUFS; i++) {
+    if (ctx->tail_busy[i]) continue;
+    void*& b = ctx->tail_pinned[i];
+    if (!b) {
+      hipError_t e = hipHostMalloc(&b, CAP, hipHostMallocDefault);
+      if (e != hipSuccess) {
+        b = nullptr;
+        set_error(std::string("hipHostMalloc: ") + hipGetErrorString(e));
+        return GM_ERR_OOM;
+      }
     }
+    ctx->tail_busy[i] = true;
+    *out = static_cast<uint8_t*>(b);
+    *idx = i;
+    return GM_OK;
   }
-  *out = static_cast<uint8_t*>(b);
-  return GM_OK;
+  set_error("msm: more than " + std::to_string(gm_ctx::TAIL_BUFS) + " MSM readbacks pending on one context");
+  return GM_ERR_INVALID;
+}
+inline void tail_pinned_release(gm_ctx* ctx, int idx) {
+  if (ctx && idx >= 0 && idx < gm_ctx::TAIL_BUFS) ctx->tail_busy[idx] = false;
 }
 
 // Pinned host staging of at least `bytes` (grown on demand; freed by gm_destroy).

@@ -25,6 +25,7 @@ import (
 	"errors"
 	"fmt"
 	"os"
+	"runtime"
 	"strconv"
 	"strings"
 	"sync"
@@ -136,24 +137,53 @@ func boolsToBytes(b []bool) []byte {
 	return out
 }
 
+// cHost fills the C-ABI's gm_g16_pk_host from k.  cgo rule: &h is a Go pointer
+// handed to C, so every Go pointer stored IN h must be pinned for the call
+// (runtime.Pinner, Go >= 1.21; the reference pins Go 1.22, go.mod:3) -- without
+// it the default GODEBUG=cgocheck=1 panics with "cgo argument has Go pointer to
+// unpinned Go pointer".  The caller unpins after the C call returns; the library
+// never keeps these pointers (include/gnark_mi355x.h).  withPoints=false leaves
+// the point-array fields nil (the dump upload reads them from the file).
+func (k *G16HostKey) cHost(pin *runtime.Pinner, withPoints bool) C.gm_g16_pk_host {
+	pinned := func(p unsafe.Pointer) unsafe.Pointer {
+		if p != nil {
+			pin.Pin(p)
+		}
+		return p
+	}
+	h := C.gm_g16_pk_host{
+		domain_size: C.size_t(k.DomainSize), nb_wires: C.size_t(k.NbWires), nb_public: C.size_t(k.NbPublic),
+		nbA: C.size_t(k.NbA), nbB: C.size_t(k.NbB), nbK: C.size_t(k.NbK),
+		g1_alpha: pinned(k.Alpha), g1_beta: pinned(k.Beta), g1_delta: pinned(k.Delta),
+		g2_beta: pinned(k.Beta2), g2_delta: pinned(k.Delta2),
+	}
+	if withPoints {
+		h.g1_A, h.g1_B, h.g1_Z, h.g1_K = pinned(k.A), pinned(k.B), pinned(k.Z), pinned(k.K)
+		h.g2_B = pinned(k.B2)
+	}
+	if len(k.InfA) > 0 {
+		infA := boolsToBytes(k.InfA)
+		h.infA = (*C.uint8_t)(pinned(unsafe.Pointer(&infA[0])))
+	}
+	if len(k.InfB) > 0 {
+		infB := boolsToBytes(k.InfB)
+		h.infB = (*C.uint8_t)(pinned(unsafe.Pointer(&infB[0])))
+	}
+	if len(k.KWires) > 0 {
+		h.k_wires = (*C.uint32_t)(pinned(unsafe.Pointer(&k.KWires[0])))
+	}
+	return h
+}
+
 // UploadG16Key uploads k once (sharded across the GPUs when there are several).
 func UploadG16Key(curve int, k *G16HostKey, flags uint) (*G16Key, error) {
 	ctx, err := Ctx()
 	if err != nil {
 		return nil, err
 	}
-	infA, infB := boolsToBytes(k.InfA), boolsToBytes(k.InfB)
-	h := C.gm_g16_pk_host{
-		domain_size: C.size_t(k.DomainSize), nb_wires: C.size_t(k.NbWires), nb_public: C.size_t(k.NbPublic),
-		nbA: C.size_t(k.NbA), nbB: C.size_t(k.NbB), nbK: C.size_t(k.NbK),
-		g1_alpha: k.Alpha, g1_beta: k.Beta, g1_delta: k.Delta,
-		g1_A: k.A, g1_B: k.B, g1_Z: k.Z, g1_K: k.K,
-		g2_beta: k.Beta2, g2_delta: k.Delta2, g2_B: k.B2,
-		infA: (*C.uint8_t)(unsafe.Pointer(&infA[0])), infB: (*C.uint8_t)(unsafe.Pointer(&infB[0])),
-	}
-	if len(k.KWires) > 0 {
-		h.k_wires = (*C.uint32_t)(unsafe.Pointer(&k.KWires[0]))
-	}
+	var pin runtime.Pinner
+	defer pin.Unpin()
+	h := k.cHost(&pin, true)
 	key := &G16Key{curve: C.int(curve)}
 	if multi != nil {
 		if rc := C.gm_g16_pk_upload_multi(multi, C.int(curve), &h, C.uint(flags), &key.multi); rc != C.GM_OK {
@@ -207,17 +237,9 @@ func UploadG16KeyDump(curve int, k *G16HostKey, f *os.File, offset int64, flags 
 	if multi != nil {
 		return nil, 0, errors.New("gnark_mi355x: dump streaming drives one device; use UploadG16Key with several")
 	}
-	infA, infB := boolsToBytes(k.InfA), boolsToBytes(k.InfB)
-	h := C.gm_g16_pk_host{
-		domain_size: C.size_t(k.DomainSize), nb_wires: C.size_t(k.NbWires), nb_public: C.size_t(k.NbPublic),
-		nbA: C.size_t(k.NbA), nbB: C.size_t(k.NbB), nbK: C.size_t(k.NbK),
-		g1_alpha: k.Alpha, g1_beta: k.Beta, g1_delta: k.Delta,
-		g2_beta: k.Beta2, g2_delta: k.Delta2,
-		infA: (*C.uint8_t)(unsafe.Pointer(&infA[0])), infB: (*C.uint8_t)(unsafe.Pointer(&infB[0])),
-	}
-	if len(k.KWires) > 0 {
-		h.k_wires = (*C.uint32_t)(unsafe.Pointer(&k.KWires[0]))
-	}
+	var pin runtime.Pinner
+	defer pin.Unpin()
+	h := k.cHost(&pin, false) // the point arrays come from the file
 	key := &G16Key{curve: C.int(curve)}
 	var end C.uint64_t
 	if rc := C.gm_g16_pk_upload_dump(ctx, C.int(curve), &h, C.int(f.Fd()), C.uint64_t(offset), C.uint(flags), &end,

@@ -80,17 +80,18 @@ func (pk *ProvingKey) setupDevicePointers(r1cs *cs.R1CS) error {
 		InfA:     pk.InfinityA, InfB: pk.InfinityB,
 		KWires:   kWires(r1cs, nbWires),
 	}
-	first := func(n int, p unsafe.Pointer) unsafe.Pointer {
-		if n == 0 {
+	// &s[0] of an empty slice would panic before any length test: take the
+	// address only when there is an element
+	g1 := func(s []curve.G1Affine) unsafe.Pointer {
+		if len(s) == 0 {
 			return nil
 		}
-		return p
+		return unsafe.Pointer(&s[0])
 	}
-	k.A = first(len(pk.G1.A), unsafe.Pointer(&pk.G1.A[0]))
-	k.B = first(len(pk.G1.B), unsafe.Pointer(&pk.G1.B[0]))
-	k.Z = first(len(pk.G1.Z), unsafe.Pointer(&pk.G1.Z[0]))
-	k.K = first(len(pk.G1.K), unsafe.Pointer(&pk.G1.K[0]))
-	k.B2 = first(len(pk.G2.B), unsafe.Pointer(&pk.G2.B[0]))
+	k.A, k.B, k.Z, k.K = g1(pk.G1.A), g1(pk.G1.B), g1(pk.G1.Z), g1(pk.G1.K)
+	if len(pk.G2.B) > 0 {
+		k.B2 = unsafe.Pointer(&pk.G2.B[0])
+	}
 	flags := uint(0)
 	if precomputeRequested() {
 		flags |= gm.PkPrecompute
