@@ -234,6 +234,13 @@ int gm_set_msm_window(gm_ctx* ctx, int c) {
   return GM_OK;
 }
 
+int gm_set_msm_glv(gm_ctx* ctx, int mode) {
+  if (!ctx || mode < -1 || mode > 1) return GM_ERR_INVALID;
+  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  ctx->msm_glv = mode;
+  return GM_OK;
+}
+
 // ---- memory -----------------------------------------------------------------
 int gm_malloc(gm_ctx* ctx, size_t bytes, void** dev_out) {
   std::lock_guard<std::recursive_mutex> g(ctx->mu);
@@ -303,6 +310,11 @@ int gm_msm(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const void* 
 }
 
 }  // extern "C"
+
+bool gm::msm_glv_on(const gm_ctx* ctx, bool g2) {
+  if (ctx && ctx->msm_glv >= 0) return ctx->msm_glv != 0;
+  return msm_glv_enabled() && (!g2 || msm_glv_g2_enabled());
+}
 
 // MsmTail's pinned readback buffer goes back to its context (msm.hpp)
 void gm::MsmTail::release_stage() {
@@ -409,6 +421,7 @@ int gm_msm_wait(gm_msm_pending* p, void* out_jac, void* out_affine) {
 
 int gm_msm_host_scalars(gm_ctx* ctx, int curve, int g2, const void* scalars_host,
                         const void* points_dev, size_t n, void* out_jac, void* out_affine) {
+  if (!ctx || (n && !scalars_host)) return GM_ERR_INVALID;
   std::lock_guard<std::recursive_mutex> g(ctx->mu);
   GM_HIP(hipSetDevice(ctx->device));
   Arena arena(ctx);
@@ -497,6 +510,7 @@ static int make_precomp(int curve, size_t n, int window, MsmPrecomp* out) {
   }
   out->c = (uint32_t)window;
   out->W = (uint32_t)((bits + 1 + window - 1) / window);
+  out->narrow = precomp_narrow(out->c, out->W, bits);
   out->stride = n;
   return GM_OK;
 }

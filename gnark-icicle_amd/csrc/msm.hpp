@@ -35,10 +35,26 @@ int msm_sort_digits(gm_ctx* ctx, Arena& arena, const SortGeom& g, size_t n, uint
 // accumulation work is unchanged (one mixed add per non-zero digit), but the
 // bucket reduction runs once instead of W times, which lets c grow (fewer
 // windows).  c == 0 means plain points (no precomputation).
+// Version of the precomputed-copy rule below (part of the device-layout cache
+// fingerprint, pk_io.hip): bump when the copies' content or order changes.
+// Layout 2: the last `narrow` windows are c - 1 bits wide so that the windows
+// cover exactly bits + 1 bits: with one shared bucket set, a narrow TOP window
+// (e.g. 13 of 22 bits at 2^24) would pile n / 2^12 entries on each of the
+// lowest 2^12 buckets (long slice spans, tree fixups, hot sort bins); spreading
+// the excess one bit per window keeps every bucket within ~2x of the mean.
+constexpr uint32_t PRECOMP_LAYOUT = 2;
 struct MsmPrecomp {
   uint32_t c = 0, W = 0;
+  uint32_t narrow = 0;  // windows W - narrow .. W - 1 are c - 1 bits wide
   size_t stride = 0;
 };
+// narrow windows of a (c, W) layout over `bits`-bit scalars: c W - narrow =
+// bits + 1 (signed digits), at least one full-width window
+inline uint32_t precomp_narrow(uint32_t c, uint32_t W, int bits) {
+  const long long e = (long long)c * W - (bits + 1);
+  if (e <= 0) return 0;
+  return (uint32_t)(e < (long long)W - 1 ? e : (long long)W - 1);
+}
 
 // Window size and copy count for a precomputed set of n points of a
 // `bits`-bit scalar field: minimises n*W accumulation adds + ~3 adds per bucket.
@@ -53,27 +69,31 @@ struct MsmPlan {
   size_t n = 0, M = 0;  // M: upper bound on the sorted entries (n * W); offsets[total] = actual
   size_t npts = 0;    // points addressable through the plan (bounds check)
   int bits = 0;       // scalar bits the digits cover (FR_BITS; 127 for a GLV split)
+  uint32_t wn = 0;    // first narrow window (window_geom; W when all are c bits)
   uint32_t* keys = nullptr;     // sorted bucket keys (window-major bucket index), offsets[total] entries
   uint32_t* vals = nullptr;     // point index | sign << 31
   uint32_t* offsets = nullptr;  // total + 1 bucket start offsets
 };
-// glv (BN254 plain layout only): each scalar k is split k = k1 + k2 lambda with
-// |k1|, |k2| < 2^127, over 2n points [P_0..P_{n-1}, phi(P_0)..phi(P_{n-1})]
-// (msm_device_launch builds them): half the windows, so half the buckets to
-// reduce, for the same number of bucket adds.
+// glv (plain layout, BN254 and BLS12-377): each scalar k is split
+// k = k1 + k2 lambda with |k1|, |k2| < 2^127, over 2n points
+// [P_0..P_{n-1}, phi(P_0)..phi(P_{n-1})] (msm_device_launch builds them): half
+// the windows, so half the buckets to reduce, for the same number of bucket adds.
 template <class C>
 int msm_plan(gm_ctx* ctx, Arena& arena, const void* scalars_dev, size_t n, const MsmPrecomp* pre,
              MsmPlan& plan, bool glv = false);
-// GLV used for plain BN254 G1 MSMs from gnark-layout points (GM_MSM_GLV=0 disables)
+// GLV used for plain MSMs from gnark-layout points (GM_MSM_GLV=0 disables)
 inline bool msm_glv_enabled() {
   static const bool on = !(getenv("GM_MSM_GLV") && getenv("GM_MSM_GLV")[0] == '0');
   return on;
 }
-// ... and for BN254 G2 (phi(x, y) = (beta^2 x, y) on the twist; GM_MSM_GLV_G2=0 disables)
+// ... and for G2 (phi(x, y) = (beta^2 x, y) on the twist; GM_MSM_GLV_G2=0 disables)
 inline bool msm_glv_g2_enabled() {
   static const bool on = !(getenv("GM_MSM_GLV_G2") && getenv("GM_MSM_GLV_G2")[0] == '0');
   return on;
 }
+// GLV for an MSM on ctx: the context's setting (gm_set_msm_glv) or, by
+// default, the environment's (GM_MSM_GLV / GM_MSM_GLV_G2)
+bool msm_glv_on(const gm_ctx* ctx, bool g2);
 template <class C, bool G2>
 int msm_run(gm_ctx* ctx, const MsmPlan& plan, const void* points_internal,
             typename GroupSel<C, G2>::HF (&jac_out)[3]);

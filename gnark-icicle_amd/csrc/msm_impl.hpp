@@ -60,9 +60,17 @@ GM_DEV FeG<Fr> load_scalar_canonical(const uint32_t* __restrict__ s, uint32_t i)
 // Plain layout: bucket b = w*nb + |d|-1 (window-major), entry value = point
 // index | sign << 31.  Precomputed (shared-bucket) layout: b = |d|-1 for every
 // window, value = w*stride + i (the shifted copy) | sign << 31.
+// Windows 0..wn-1 are c bits wide, windows wn..W-1 (the `narrow` windows of a
+// precomputed layout, msm.hpp MsmPrecomp) c - 1 bits; plain layouts: wn = W.
 struct DigitGeom {
   uint32_t n, c, W, nb, shared_stride, F;  // F: pass-1 bin = b >> F
+  uint32_t wn;
 };
+// bit offset and width of window w
+GM_HD void window_geom(uint32_t c, uint32_t wn, uint32_t w, uint32_t& off, uint32_t& cw) {
+  off = w * c - (w > wn ? w - wn : 0u);
+  cw = w >= wn ? c - 1 : c;
+}
 
 // ---------------------------------------------------------------------------
 // Bucket sort of the digits: a two-level counting sort written for this job.
@@ -95,13 +103,14 @@ __global__ void __launch_bounds__(1024) k_msm_digits(const uint32_t* __restrict_
     const uint32_t i = base + r * DG_THREADS + t;
     if (i >= g.n) break;
     const FeG<Fr> k = load_scalar_canonical<Fr>(scalars, i);
-    const uint32_t mask = (1u << g.c) - 1;
     uint32_t carry = 0;
     for (uint32_t w = 0; w < g.W; w++) {
-      const uint32_t raw = window_bits(k, w * g.c, mask) + carry;
+      uint32_t off, cw;
+      window_geom(g.c, g.wn, w, off, cw);
+      const uint32_t raw = window_bits(k, off, (1u << cw) - 1) + carry;
       uint32_t d, neg;
-      if (raw > g.nb) {
-        d = (1u << g.c) - raw;
+      if (raw > (1u << (cw - 1))) {
+        d = (1u << cw) - raw;
         carry = 1;
         neg = 1;
       } else {
@@ -159,18 +168,63 @@ struct GlvBn254 {
   }
 };
 
+// ---------------------------------------------------------------------------
+// GLV split for BLS12-377: lambda = x^2 - 1 (x = 0x8508c00000000001, the curve
+// seed) is a cube root of unity mod r with lambda^2 < r < (lambda + 1)^2, so
+// k = k1 + k2 lambda with k2 = floor(k / lambda), k1 = k mod lambda -- both in
+// [0, 2^127), no signs.  q = floor(k g / 2^384), g = floor(2^384 / lambda),
+// undershoots k / lambda by less than one: one conditional correction.
+// phi(x, y) = (beta x, y) on G1, (beta^2 x, y) on the G2 twist (tools/glv_constants.py
+// checks both against the oracle's group law).
+// ---------------------------------------------------------------------------
+struct GlvBls377 {
+  GM_HD static constexpr uint64_t g(int i) {
+    constexpr uint64_t a[5] = {0x5cc5a03b7b820d29ull, 0x3366fc876f25c6b5ull, 0x7f72ed32af90182cull,
+                               0xb3f7aa969fd37160ull, 0x0000000000000003ull};
+    return a[i];
+  }
+  static constexpr uint64_t LAM_LO = 0x0a11800000000000ull, LAM_HI = 0x452217cc90000001ull;
+  GM_HD static constexpr uint32_t beta29(int i) {
+    constexpr uint32_t a[14] = {0x1c8a7893u, 0x0b7d08f2u, 0x06b88506u, 0x162aa2edu, 0x1c5fdf80u,
+                                0x11b95a22u, 0x03b86dd7u, 0x1191f770u, 0x10701220u, 0x1501c11fu,
+                                0x1cee88bbu, 0x118d05ecu, 0x06f2fa26u, 0x00000000u};
+    return a[i];
+  }
+  GM_HD static constexpr uint32_t beta29_g2(int i) {
+    constexpr uint32_t a[14] = {0x098a903fu, 0x0deef70eu, 0x0bd62e43u, 0x12fc3bfau, 0x0de940feu,
+                                0x047b8e82u, 0x17ec1b27u, 0x1a776815u, 0x120a67b5u, 0x0a70d0c4u,
+                                0x0271dc9au, 0x182f7308u, 0x19602487u, 0x00000000u};
+    return a[i];
+  }
+};
+
+// beta of phi per base field: g1 for G1 points, g2 (= beta^2) for the G2 twist
+template <class P>
+struct GlvBeta;
+template <>
+struct GlvBeta<Bn254Fp> {
+  GM_HD static constexpr uint32_t g1(int i) { return GlvBn254::beta29(i); }
+  GM_HD static constexpr uint32_t g2(int i) { return GlvBn254::beta29_g2(i); }
+};
+template <>
+struct GlvBeta<Bls377Fp> {
+  GM_HD static constexpr uint32_t g1(int i) { return GlvBls377::beta29(i); }
+  GM_HD static constexpr uint32_t g2(int i) { return GlvBls377::beta29_g2(i); }
+};
+
 // x -> beta x of the GLV endomorphism, G1 (Fp) and G2 (Fp2, beta in Fp)
-GM_DEV Fe<Bn254Fp> glv_phi_x(const Fe<Bn254Fp>& x) {
-  Fe<Bn254Fp> b;
+template <class P>
+GM_DEV Fe<P> glv_phi_x(const Fe<P>& x) {
+  Fe<P> b;
 #pragma unroll
-  for (int j = 0; j < Bn254Fp::N; j++) b.v[j] = GlvBn254::beta29(j);
+  for (int j = 0; j < P::N; j++) b.v[j] = GlvBeta<P>::g1(j);
   return fe_mul(x, b);
 }
-template <int B>
-GM_DEV Fe2<Bn254Fp, B> glv_phi_x(const Fe2<Bn254Fp, B>& x) {
-  Fe<Bn254Fp> b;
+template <class P, int B>
+GM_DEV Fe2<P, B> glv_phi_x(const Fe2<P, B>& x) {
+  Fe<P> b;
 #pragma unroll
-  for (int j = 0; j < Bn254Fp::N; j++) b.v[j] = GlvBn254::beta29_g2(j);
+  for (int j = 0; j < P::N; j++) b.v[j] = GlvBeta<P>::g2(j);
   return {fe_mul(x.a0, b), fe_mul(x.a1, b)};
 }
 
@@ -215,12 +269,54 @@ GM_DEV void emit_digits(const FeG<Fr>& k, uint32_t flip, uint32_t i, const Digit
   }
 }
 
+// Scalar split k = k1 + k2 lambda per curve: k1 in [0, 2^127), |k2| < 2^127,
+// neg2 = sign of k2 (BLS12-377: always 0).
+template <class C>
+struct Glv {
+  static constexpr bool ok = false;
+};
+template <>
+struct Glv<CurveBN254> {
+  static constexpr bool ok = true;
+  using U = unsigned __int128;
+  GM_DEV static void split(const uint64_t (&k64)[4], U& k1, U& k2, uint32_t& neg2) {
+    const U c1 = glv_mulshift<5>(k64, GlvBn254::g1);
+    const U c2 = glv_mulshift<4>(k64, GlvBn254::g2);
+    const U a1 = ((U)GlvBn254::A1_HI << 64) | GlvBn254::A1_LO;
+    const U b2 = ((U)GlvBn254::B2_HI << 64) | GlvBn254::B2_LO;
+    const U klo = ((U)k64[1] << 64) | k64[0];
+    k1 = klo - c1 * a1 - c2 * (U)GlvBn254::A2;  // in [0, 2^127)
+    k2 = c1 * (U)GlvBn254::A2 - c2 * b2;        // signed, |k2| < 2^127
+    neg2 = (uint32_t)(k2 >> 127);
+    if (neg2) k2 = (U)0 - k2;
+  }
+};
+template <>
+struct Glv<CurveBLS12377> {
+  static constexpr bool ok = true;
+  using U = unsigned __int128;
+  GM_DEV static void split(const uint64_t (&k64)[4], U& k1, U& k2, uint32_t& neg2) {
+    U q = glv_mulshift<5>(k64, GlvBls377::g);  // floor(k / lambda) or one less
+    const U lam = ((U)GlvBls377::LAM_HI << 64) | GlvBls377::LAM_LO;
+    const U klo = ((U)k64[1] << 64) | k64[0];
+    U r = klo - q * lam;  // true value in [0, 2 lambda): exact mod 2^128
+    if (r >= lam) {
+      r -= lam;
+      q += 1;
+    }
+    k1 = r;
+    k2 = q;
+    neg2 = 0;
+  }
+};
+
 // k_msm_digits for the GLV split (plain layout): thread i writes the digits of
 // k1 at virtual point i and of k2 at virtual point n0 + i (g.n = 2 n0).
-template <int Unused = 0>
+template <class C>
 __global__ void __launch_bounds__(1024) k_msm_digits_glv(const uint32_t* __restrict__ scalars, DigitGeom g,
                                                          uint32_t n0, uint32_t NC, uint32_t* __restrict__ dig,
                                                          uint32_t* __restrict__ ccount) {
+  using Fr = typename C::Fr;
   extern __shared__ uint32_t dg_lds[];
   const uint32_t t = threadIdx.x;
   for (uint32_t q = t; q < NC; q += DG_THREADS) dg_lds[q] = 0;
@@ -229,36 +325,29 @@ __global__ void __launch_bounds__(1024) k_msm_digits_glv(const uint32_t* __restr
   for (uint32_t r = 0; r < DG_PPT; r++) {
     const uint32_t i = base + r * DG_THREADS + t;
     if (i >= n0) break;
-    const FeG<Bn254Fr> k = load_scalar_canonical<Bn254Fr>(scalars, i);
+    const FeG<Fr> k = load_scalar_canonical<Fr>(scalars, i);
     uint64_t k64[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) k64[j] = (uint64_t)k.w[2 * j] | ((uint64_t)k.w[2 * j + 1] << 32);
-    using U = unsigned __int128;
-    const U c1 = glv_mulshift<5>(k64, GlvBn254::g1);
-    const U c2 = glv_mulshift<4>(k64, GlvBn254::g2);
-    const U a1 = ((U)GlvBn254::A1_HI << 64) | GlvBn254::A1_LO;
-    const U b2 = ((U)GlvBn254::B2_HI << 64) | GlvBn254::B2_LO;
-    const U klo = ((U)k64[1] << 64) | k64[0];
-    const U k1 = klo - c1 * a1 - c2 * (U)GlvBn254::A2;  // in [0, 2^127)
-    U k2 = c1 * (U)GlvBn254::A2 - c2 * b2;               // signed, |k2| < 2^127
-    const uint32_t neg2 = (uint32_t)(k2 >> 127);
-    if (neg2) k2 = (U)0 - k2;
-    FeG<Bn254Fr> m1, m2;
+    unsigned __int128 k1, k2;
+    uint32_t neg2;
+    Glv<C>::split(k64, k1, k2, neg2);
+    FeG<Fr> m1, m2;
 #pragma unroll
-    for (int j = 0; j < Bn254Fr::NG; j++) {
+    for (int j = 0; j < Fr::NG; j++) {
       m1.w[j] = j < 4 ? (uint32_t)(k1 >> (32 * j)) : 0u;
       m2.w[j] = j < 4 ? (uint32_t)(k2 >> (32 * j)) : 0u;
     }
-    emit_digits<Bn254Fr>(m1, 0u, i, g, dig, dg_lds);
-    emit_digits<Bn254Fr>(m2, neg2, n0 + i, g, dig, dg_lds);
+    emit_digits<Fr>(m1, 0u, i, g, dig, dg_lds);
+    emit_digits<Fr>(m2, neg2, n0 + i, g, dig, dg_lds);
   }
   __syncthreads();
   for (uint32_t q = t; q < NC; q += DG_THREADS)
     if (dg_lds[q]) atomicAdd(&ccount[q], dg_lds[q]);
 }
 
-// gnark-layout BN254 G1 points -> internal layout, plus phi(P_i) = (beta x, y)
-// at n + i (the GLV point set)
+// gnark-layout points -> internal layout, plus phi(P_i) = (beta x, y) at n + i
+// (the GLV point set; G2: beta^2 on the twist)
 template <class F>
 __global__ void __launch_bounds__(256) k_msm_convert_points_glv(const uint32_t* __restrict__ src, size_t n,
                                                                 uint32_t* __restrict__ dst) {
@@ -283,12 +372,13 @@ __global__ void __launch_bounds__(256) k_msm_convert_points(const uint32_t* __re
   store_affine_packed<F>(dst + i * PW, load_affine_gnark<F>(src + i * PW));
 }
 
-// Fixed-base copies: pts[w*stride + i] = [2^(c w)] pts[i] for w = 1..W-1
-// (copy 0 already converted).  c doublings per copy in XYZZ, then one Fermat
+// Fixed-base copies: pts[w*stride + i] = [2^off(w)] pts[i] for w = 1..W-1
+// (copy 0 already converted; off(w) = window_geom's offset, windows >= wn one
+// bit narrower).  width(w-1) doublings per copy in XYZZ, then one Fermat
 // inversion back to affine; one-time setup cost, like the pk upload itself.
 template <class F>
 __global__ void __launch_bounds__(128) k_msm_precompute(uint32_t* __restrict__ pts, size_t n, size_t stride,
-                                                        uint32_t c, uint32_t W) {
+                                                        uint32_t c, uint32_t W, uint32_t wn) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   constexpr int PW = 2 * Coord<F>::WORDS;
@@ -306,7 +396,8 @@ __global__ void __launch_bounds__(128) k_msm_precompute(uint32_t* __restrict__ p
   acc.zz = FOps<F>::one();
   acc.zzz = FOps<F>::one();
   for (uint32_t w = 1; w < W; w++) {
-    for (uint32_t k = 0; k < c; k++) acc = xyzz_dbl(acc);
+    const uint32_t cw = (w - 1 >= wn) ? c - 1 : c;
+    for (uint32_t k = 0; k < cw; k++) acc = xyzz_dbl(acc);
     Affine<F> r = zero;
     if (!xyzz_is_inf(acc)) {
       const F t = fe_inv(fe_mul(acc.zz, acc.zzz));
@@ -690,8 +781,8 @@ int msm_plan(gm_ctx* ctx, Arena& arena, const void* scalars_dev, size_t n, const
   plan.n = n;
   plan.bits = C::FR_BITS;
   if (n == 0) return GM_OK;
-  if (glv && (!std::is_same<typename C::Fr, Bn254Fr>::value || (pre && pre->c))) {
-    set_error("msm: the GLV split is BN254 plain-layout only");
+  if (glv && (!Glv<C>::ok || (pre && pre->c))) {
+    set_error("msm: the GLV split needs a plain (not precomputed) layout");
     return GM_ERR_INVALID;
   }
   const size_t n0 = n;  // scalars
@@ -705,8 +796,8 @@ int msm_plan(gm_ctx* ctx, Arena& arena, const void* scalars_dev, size_t n, const
     return GM_ERR_INVALID;
   }
   const bool shared = pre && pre->c;
-  if (shared && (pre->stride < n || (size_t)pre->W * pre->stride >= (size_t(1) << 31) ||
-                 (size_t)pre->c * pre->W < (size_t)C::FR_BITS + 1)) {
+  if (shared && (pre->stride < n || (size_t)pre->W * pre->stride >= (size_t(1) << 31) || pre->narrow >= pre->W ||
+                 (size_t)pre->c * pre->W - pre->narrow < (size_t)C::FR_BITS + 1)) {
     set_error("msm: precomputed point set does not cover this MSM");
     return GM_ERR_INVALID;
   }
@@ -772,13 +863,15 @@ int msm_plan(gm_ctx* ctx, Arena& arena, const void* scalars_dev, size_t n, const
   g.W = W;
   g.nb = plan.nb;
   g.shared_stride = shared ? (uint32_t)pre->stride : 0u;
+  g.wn = shared ? W - pre->narrow : W;
+  plan.wn = g.wn;
   g.F = sg.F + sg.G;  // the digits kernel counts pass-1 bins
   {
     ProfScope ps(ctx, "msm_digits");
     GM_HIP(hipMemsetAsync(scount.p, 0, sizeof(uint32_t) * sg.NS, st));
-    if constexpr (std::is_same<typename C::Fr, Bn254Fr>::value) {
+    if constexpr (Glv<C>::ok) {
       if (glv)
-        hipLaunchKernelGGL(k_msm_digits_glv<0>, dim3(blocks_for(n0, DG_THREADS * DG_PPT)), dim3(DG_THREADS),
+        hipLaunchKernelGGL(k_msm_digits_glv<C>, dim3(blocks_for(n0, DG_THREADS * DG_PPT)), dim3(DG_THREADS),
                          sizeof(uint32_t) * sg.NS, st, reinterpret_cast<const uint32_t*>(scalars_dev), g,
                            (uint32_t)n0, sg.NS, dig.as<uint32_t>(), scount.as<uint32_t>());
     }
@@ -1000,9 +1093,17 @@ int msm_launch(gm_ctx* ctx, Arena& arena, const MsmPlan& plan, const void* point
   // shared).  Large MSMs whose top window is narrow (2^24: 1024-4096 entries per
   // top digit) sync on the max span first.
   {
-    const int top_bits = plan.bits - (int)(t.c * (t.W - 1));
-    double fullest = (double)plan.n / std::ldexp(1.0, top_bits > 0 ? top_bits : 0);
-    if (t.Wr == 1 && t.W > 1) fullest += (double)(t.W - 1) * (double)plan.n / (double)t.nb;
+    // expected entries of the fullest bucket: bucket 0 gets n / h_w from window
+    // w, h_w = the largest digit of w (its width, or the bits left above it)
+    double fullest = 0;
+    for (uint32_t w = 0; w < t.W; w++) {
+      uint32_t off, cw;
+      window_geom(t.c, plan.wn, w, off, cw);
+      const int left = plan.bits - (int)off;
+      const double h = std::ldexp(1.0, std::max(0, std::min((int)cw - 1, left)));
+      const double load = (double)plan.n / h;
+      fullest = t.Wr == 1 ? fullest + load : std::max(fullest, load);
+    }
     if (fullest > 0.5 * FIX_SERIAL * t.K) {
       uint8_t* pb;
       int pbi;
@@ -1105,10 +1206,10 @@ int msm_device_launch(gm_ctx* ctx, Arena& arena, const void* scalars_dev, const 
       set_error("msm: a precomputed point set must be device-internal");
       return GM_ERR_INVALID;
     }
-    glv = std::is_same<typename C::Fr, Bn254Fr>::value && msm_glv_enabled() && (!G2 || msm_glv_g2_enabled());
+    glv = Glv<C>::ok && msm_glv_on(ctx, G2);
     if ((rc = ipts.alloc(arena, 2 * Coord<DF>::WORDS * sizeof(uint32_t) * n * (glv ? 2 : 1)))) return rc;
     ProfScope ps(ctx, "msm_convert_points");
-    if constexpr (std::is_same<typename C::Fr, Bn254Fr>::value) {
+    if constexpr (Glv<C>::ok) {
       if (glv)
         hipLaunchKernelGGL(k_msm_convert_points_glv<DF>, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream,
                            reinterpret_cast<const uint32_t*>(points_dev), n, ipts.as<uint32_t>());
@@ -1159,7 +1260,7 @@ int msm_precompute_points(gm_ctx* ctx, const void* gnark_points, size_t n, const
                      reinterpret_cast<const uint32_t*>(gnark_points), n, reinterpret_cast<uint32_t*>(dst));
   if (pre.W > 1)
     hipLaunchKernelGGL(k_msm_precompute<DF>, dim3(blocks_for(n, 128)), dim3(128), 0, ctx->stream,
-                       reinterpret_cast<uint32_t*>(dst), n, pre.stride, pre.c, pre.W);
+                       reinterpret_cast<uint32_t*>(dst), n, pre.stride, pre.c, pre.W, pre.W - pre.narrow);
   GM_HIP(hipGetLastError());
   return GM_OK;
 }

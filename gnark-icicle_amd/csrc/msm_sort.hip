@@ -447,6 +447,7 @@ MsmPrecomp msm_choose_precomp(size_t n, int bits) {
     }
   }
   best.stride = n;
+  best.narrow = precomp_narrow(best.c, best.W, bits);
   return best;
 }
 

@@ -23,7 +23,9 @@
 #include <cstring>
 #include <string>
 
+#include "curves.hpp"
 #include "groth16.hpp"
+#include "msm.hpp"
 #include "runtime.hpp"
 
 using namespace gm;
@@ -141,15 +143,48 @@ void shard_range(size_t n, int rank, int world, size_t* lo, size_t* hi) {
 
 // ---- device-layout cache ---------------------------------------------------
 constexpr char CACHE_MAGIC[8] = {'G', 'M', 'P', 'K', 'C', 'A', 'C', 'H'};
-constexpr uint32_t CACHE_VERSION = 1;
+constexpr uint32_t CACHE_VERSION = 2;
+// Device-layout fingerprint: the internal point form (radix-2^29 Montgomery
+// limbs packed in gnark's word layout) and the precomputed-copy rule
+// (PRECOMP_LAYOUT, msm.hpp).  A cache written by a build with another layout is
+// refused instead of being read as points.
+constexpr uint32_t CACHE_LAYOUT = (uint32_t(RADIX) << 24) | (uint32_t(PRECOMP_LAYOUT) << 8) | 1u;
 
 struct CacheHeader {
   char magic[8];
   uint32_t version, curve;
+  uint32_t layout, reserved;
   uint64_t n, nb_wires, nb_public, nbA, nbB, nbK, zlo, nbZ, wlo, whi, precomp;
   uint32_t pre_c[4], pre_W[4];
   uint64_t pre_stride[4];
 };
+
+// Header invariants of a device-layout cache (a corrupt or foreign header must
+// not size allocations or steer device gathers out of bounds).
+int check_cache_header(const CacheHeader& h) {
+  auto bad = [](const char* what) {
+    set_error(std::string("pk cache: inconsistent header (") + what + ")");
+    return GM_ERR_INVALID;
+  };
+  const uint64_t lim = uint64_t(1) << 31;
+  if (h.n < 2 || (h.n & (h.n - 1)) || h.n > lim) return bad("domain size");
+  if (h.nb_wires == 0 || h.nb_wires > lim || h.nb_public > h.nb_wires) return bad("wire counts");
+  if (h.zlo > h.n - 1 || h.nbZ > h.n - 1 - h.zlo) return bad("Z slice");
+  if (h.wlo > h.whi || h.whi > h.nb_wires) return bad("wire slice");
+  if (h.nbA > h.nb_wires || h.nbB > h.nb_wires || h.nbK > h.nb_wires) return bad("array lengths");
+  if (h.precomp > 1) return bad("precompute flag");
+  if (h.precomp) {
+    const int frbits = h.curve == GM_BN254 ? CurveBN254::FR_BITS : CurveBLS12377::FR_BITS;
+    const uint64_t cnt[4] = {h.nbA, h.nbB, h.nbZ, h.nbK};
+    for (int i = 0; i < 4; i++) {
+      if (h.pre_c[i] < 1 || h.pre_c[i] > 30 || h.pre_W[i] < 1 ||
+          (uint64_t)h.pre_c[i] * h.pre_W[i] < (uint64_t)frbits + 1)
+        return bad("window geometry");
+      if (h.pre_stride[i] < cnt[i] || (uint64_t)h.pre_W[i] * h.pre_stride[i] >= lim) return bad("window copies");
+    }
+  }
+  return GM_OK;
+}
 
 size_t array_bytes(const gm_g16_pk* pk, int which) {
   const size_t g1 = internal_point_bytes(pk->curve, false), g2 = internal_point_bytes(pk->curve, true);
@@ -209,15 +244,14 @@ struct gm_g16_stage {
 
 namespace {
 // dst[idx[j]] = val[j] (32-byte Fr)
+// (gm_g16_stage_put_indexed checks every index on the host before the copy;
+// the i < len test only keeps a bad launch from writing out of bounds)
 __global__ void k_scatter_fr(const uint32_t* __restrict__ idx, const uint4* __restrict__ val, size_t k, size_t len,
-                             uint4* __restrict__ dst, uint32_t* __restrict__ err) {
+                             uint4* __restrict__ dst) {
   const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= k) return;
   const size_t i = idx[j];
-  if (i >= len) {
-    atomicOr(err, 1u);
-    return;
-  }
+  if (i >= len) return;
   dst[2 * i] = val[2 * j];
   dst[2 * i + 1] = val[2 * j + 1];
 }
@@ -290,6 +324,7 @@ int gm_g16_pk_save_cache(gm_ctx* ctx, const gm_g16_pk* pk, int fd) {
   memset(&h, 0, sizeof(h));
   memcpy(h.magic, CACHE_MAGIC, 8);
   h.version = CACHE_VERSION;
+  h.layout = CACHE_LAYOUT;
   h.curve = (uint32_t)pk->curve;
   h.n = pk->n;
   h.nb_wires = pk->nb_wires;
@@ -339,7 +374,12 @@ int gm_g16_pk_load_cache(gm_ctx* ctx, int fd, gm_g16_pk** out) {
     set_error("pk cache: not a gnark_mi355x device-layout key (magic / version)");
     return GM_ERR_INVALID;
   }
+  if (h.layout != CACHE_LAYOUT) {
+    set_error("pk cache: written by a build with another device point layout");
+    return GM_ERR_INVALID;
+  }
   if ((rc = check_curve_id((int)h.curve))) return rc;
+  if ((rc = check_cache_header(h))) return rc;
   auto* pk = new gm_g16_pk();
   auto fail = [&](int code) {
     pk_release(pk);
@@ -358,9 +398,11 @@ int gm_g16_pk_load_cache(gm_ctx* ctx, int fd, gm_g16_pk** out) {
   pk->whi = h.whi;
   pk->precomp = h.precomp != 0;
   MsmPrecomp* pres[4] = {&pk->preA, &pk->preB, &pk->preZ, &pk->preK};
+  const int frbits = pk->curve == GM_BN254 ? CurveBN254::FR_BITS : CurveBLS12377::FR_BITS;
   for (int i = 0; i < 4; i++) {
     pres[i]->c = h.pre_c[i];
     pres[i]->W = h.pre_W[i];
+    pres[i]->narrow = precomp_narrow(h.pre_c[i], h.pre_W[i], frbits);  // layout 2 (CACHE_LAYOUT)
     pres[i]->stride = h.pre_stride[i];
   }
   const size_t g1b = 2 * fp_bytes(pk->curve), g2b = 4 * fp_bytes(pk->curve);
@@ -383,10 +425,21 @@ int gm_g16_pk_load_cache(gm_ctx* ctx, int fd, gm_g16_pk** out) {
       set_error("pk cache: hipMalloc failed");
       return fail(GM_ERR_OOM);
     }
+    // the compaction maps (arrays 5-7) index the wire slice: k_gather_fr reads
+    // wires[idx] unchecked, so every entry is checked here on the host
+    const uint32_t wspan = (uint32_t)(pk->whi - pk->wlo);
     for (size_t o = 0, k = 0; o < bytes; o += IO_CHUNK, k ^= 1) {
       const size_t cnt = std::min(IO_CHUNK, bytes - o);
       if ((rc = ring.acquire((int)k))) return fail(rc);
       if ((rc = read_seq(fd, ring.host[k], cnt))) return fail(rc);
+      if (a >= 5) {
+        const uint32_t* ix = (const uint32_t*)ring.host[k];
+        for (size_t j = 0; j < cnt / 4; j++)
+          if (ix[j] >= wspan) {
+            set_error("pk cache: compaction index outside the wire slice");
+            return fail(GM_ERR_INVALID);
+          }
+      }
       if (hipMemcpyAsync((char*)*dst + o, ring.host[k], cnt, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
           hipEventRecord(ring.ev[k], ctx->stream) != hipSuccess) {
         set_error("pk cache: H2D failed");
@@ -423,7 +476,7 @@ int gm_g16_stage_begin(gm_ctx* ctx, gm_g16_pk* pk, size_t nb_constraints, gm_g16
   }
   for (int i = 0; i < gm_g16_stage::SLOTS; i++) {
     if (hipHostMalloc(&st->host[i], gm_g16_stage::SLOT, hipHostMallocDefault) != hipSuccess ||
-        hipMalloc(&st->dev[i], gm_g16_stage::SLOT + 16) != hipSuccess ||
+        hipMalloc(&st->dev[i], gm_g16_stage::SLOT) != hipSuccess ||
         hipEventCreateWithFlags(&st->ev[i], hipEventDisableTiming) != hipSuccess) {
       delete st;
       set_error("stage: staging allocation failed");
@@ -484,7 +537,7 @@ int gm_g16_stage_put_indexed(gm_g16_stage* st, int which, const void* host_base,
     GM_HIP(hipMemcpyAsync(di, hi, 4 * cnt, hipMemcpyHostToDevice, ctx->copy));
     GM_HIP(hipMemcpyAsync(dv, hv, 32 * cnt, hipMemcpyHostToDevice, ctx->copy));
     hipLaunchKernelGGL(k_scatter_fr, dim3(blocks_for(cnt, 256)), dim3(256), 0, ctx->copy, di, (const uint4*)dv, cnt,
-                       st->len[which], (uint4*)st->vec[which], (uint32_t*)((char*)st->dev[s] + gm_g16_stage::SLOT));
+                       st->len[which], (uint4*)st->vec[which]);
     GM_HIP(hipGetLastError());
     GM_HIP(hipEventRecord(st->ev[s], ctx->copy));
   }

@@ -65,6 +65,7 @@ struct gm_ctx {
   std::map<int, void*> ntt_domains;
   int msm_c_override = 0;
   int msm_slice = 0;  // entries per thread in the bucket accumulation (0 = default)
+  int msm_glv = -1;   // GLV split of plain MSMs: -1 = environment default, 0 off, 1 on
   // workspace arena (stack-discipline scopes), plus two more for MSMs whose host
   // tail is deferred (pipelined MSMs: gm_msm_async, the Groth16 MSM sequence)
   gm::ArenaState arena;

@@ -41,7 +41,7 @@ FR_BYTES = 32
 SYMBOLS = [
     "gm_last_error", "gm_version", "gm_init", "gm_destroy", "gm_synchronize",
     "gm_profile_enable", "gm_profile_reset", "gm_profile_get", "gm_profile_dump",
-    "gm_set_msm_window", "gm_malloc", "gm_free", "gm_copy_to_device", "gm_memcpy_h2d",
+    "gm_set_msm_window", "gm_set_msm_glv", "gm_malloc", "gm_free", "gm_copy_to_device", "gm_memcpy_h2d",
     "gm_memcpy_d2h", "gm_memcpy_d2d", "gm_copy_points_to_device", "gm_msm", "gm_msm_host_scalars", "gm_points_upload", "gm_msm_prepared", "gm_precompute_layout", "gm_points_upload_precomputed",
     "gm_msm_precomputed", "gm_kzg_commit", "gm_ntt",
     "gm_poly_ops", "gm_reverse_scalars", "gm_groth16_compute_h", "gm_g16_pk_upload", "gm_g16_pk_upload_ex", "gm_g16_pk_upload_shard",
@@ -83,6 +83,7 @@ def load_library(path: str = LIB_PATH):
     L.gm_profile_get.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64)]
     L.gm_profile_dump.argtypes = [vp, ctypes.c_char_p, sz]
     L.gm_set_msm_window.argtypes = [vp, i]
+    L.gm_set_msm_glv.argtypes = [vp, i]
     L.gm_malloc.argtypes = [vp, sz, pvp]
     L.gm_free.argtypes = [vp, vp]
     L.gm_copy_to_device.argtypes = [vp, vp, sz, pvp]
@@ -283,6 +284,10 @@ class Context:
 
     def set_msm_window(self, c: int):
         _check(load_library().gm_set_msm_window(self.handle, c))
+
+    def set_msm_glv(self, mode: int):
+        """GLV split of plain MSMs: 1 on, 0 off, -1 environment default."""
+        _check(load_library().gm_set_msm_glv(self.handle, mode))
 
     # ---- MSM -----------------------------------------------------------------
     def msm(self, curve, scalars: DeviceBuffer, points: DeviceBuffer, n: int, g2: bool = False):
@@ -534,7 +539,9 @@ def _pk_host_struct(curve, pk: dict, domain_size: int, nb_wires: int, nb_public:
     shard = (rank, world): point arrays are sliced to the rank's shard unless
     pk_is_shard (they already are; the counts then come from pk['shard_sizes'])."""
     g1b, g2b = point_bytes(curve, False), point_bytes(curve, True)
-    arrs = {k: _buf(v) for k, v in pk.items() if k not in ("sizes", "shard_sizes", "k_wires")}
+    keys = ("g1_alpha", "g1_beta", "g1_delta", "g1_A", "g1_B", "g1_Z", "g1_K", "g2_beta", "g2_delta", "g2_B",
+            "infA", "infB")
+    arrs = {k: _buf(pk[k]) for k in keys}
     h = _PkHost()
     h.domain_size, h.nb_wires, h.nb_public = domain_size, nb_wires, nb_public
     if pk_is_shard:

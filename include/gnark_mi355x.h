@@ -17,7 +17,9 @@
  *  - Every function returns GM_OK (0) or a negative gm_status; the message of
  *    the last failure on the calling thread is available from gm_last_error().
  *  - Calls on one context are serialised; use one context per thread/GPU for
- *    concurrency (one process per GPU in multi-GPU jobs).
+ *    concurrency.  Multi-GPU: either one process drives every GPU through one
+ *    gm_multi handle: gm_g16_pk_upload_multi / gm_g16_prove_multi, or one process per
+ *    GPU holds a key shard (gm_g16_pk_upload_shard / gm_g16_prove_partial).
  */
 #ifndef GNARK_MI355X_H
 #define GNARK_MI355X_H
@@ -59,6 +61,11 @@ int gm_profile_get(gm_ctx* ctx, const char* name, double* total_ms, uint64_t* co
 int gm_profile_dump(gm_ctx* ctx, char* buf, size_t cap);
 /* Test/tuning knob: force the MSM window size c (0 = automatic). */
 int gm_set_msm_window(gm_ctx* ctx, int c);
+/* GLV split (k = k1 + k2 lambda over P_i and phi(P_i), BN254 and BLS12-377) of
+ * MSMs over gnark-layout points: mode 1 on, 0 off, -1 default (on unless
+ * GM_MSM_GLV=0; G2 also unless GM_MSM_GLV_G2=0).  Tuning / A-B knob; results
+ * are identical either way. */
+int gm_set_msm_glv(gm_ctx* ctx, int mode);
 
 /* ---- memory (iciclegnark CopyToDevice / CopyPointsToDevice /
  *      CopyG2PointsToDevice / FreeDevicePointer; icicle.go:44,47,65,90,95,
@@ -82,16 +89,19 @@ int gm_copy_points_to_device(gm_ctx* ctx, int curve, int g2, const void* host_po
  * layout; out_affine (optional, may be NULL) receives the affine form. */
 int gm_msm(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const void* points_dev,
            size_t n, void* out_jac, void* out_affine);
-/* Same with scalars in host memory (copied on the context stream). */
 /* Pipelined MSM: gm_msm_async queues the device work of gm_msm (same
  * arguments) and returns at once; gm_msm_wait finishes it (host tail: checks
  * and the Horner combination) and frees the handle.  The host tail of one MSM
  * thus overlaps the device work of the next one issued before it.  At most two
- * MSMs may be in flight per context; wait in issue order. */
+ * MSMs may be in flight per context; wait in issue order.  Synchronous calls
+ * (gm_msm, gm_msm_prepared, gm_ntt, ...) may be made on the same context while
+ * async MSMs are pending: each pending MSM keeps its own scratch arena and its
+ * own pinned readback buffer until its gm_msm_wait. */
 typedef struct gm_msm_pending gm_msm_pending;
 int gm_msm_async(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const void* points_dev, size_t n,
                  gm_msm_pending** out);
 int gm_msm_wait(gm_msm_pending* pending, void* out_jacobian, void* out_affine);
+/* gm_msm with the scalars in host memory (copied on the context stream). */
 int gm_msm_host_scalars(gm_ctx* ctx, int curve, int g2, const void* scalars_host,
                         const void* points_dev, size_t n, void* out_jac, void* out_affine);
 

@@ -20,7 +20,8 @@
 //                      A/B compaction (:157-178), deltas (:195), Ar (:213-224), Bs1 (:200-211),
 //                      Krs (:227-280), Bs (:283-305).
 //   o_g16_check        The verification equation in the exponent (equivalent to verify.go:49-150's
-//                      pairing check for a setup whose toxic waste is known).
+//                      pairing check for a setup whose toxic waste is known); o_g16_check_mask
+//                      with the BSB22 verifier-side wire set (commitment + committed wires).
 //
 // Parity status: no MSM / NTT / H known-answer vectors exist in the reference
 //  -> "parity unpinned" at the gnark-crypto boundary.  This file is
@@ -554,8 +555,13 @@ int g16_prove(const PkView<C>& pk, size_t nb_public, const uint8_t* wires, const
 
 // exponent-level verification for a known toxic waste
 template <class C>
+// vk_mask (optional, one byte per wire): the wires on the verifier's side of
+// the equation -- the public ones by default; with BSB22 commitments also the
+// commitment wires (setup.go:181-186, vkK) and the private committed ones
+// (their K terms move into the commitments D_i, verify.go:121-123).
 int g16_check(const R1csView& rv, const Toxic<C>& tw, const uint8_t* wires, const uint8_t* r_mont,
-              const uint8_t* s_mont, const uint8_t* ar, const uint8_t* bs, const uint8_t* krs) {
+              const uint8_t* s_mont, const uint8_t* ar, const uint8_t* bs, const uint8_t* krs,
+              const uint8_t* vk_mask = nullptr) {
   using Fr = typename C::Fr;
   using G1F = typename C::G1F;
   using G2F = typename C::G2F;
@@ -569,7 +575,7 @@ int g16_check(const R1csView& rv, const Toxic<C>& tw, const uint8_t* wires, cons
     Fe<Fr> w = load_fe<Fr>(wires + 32 * i);
     sa = add(sa, mul(w, abc[0][i]));
     sb = add(sb, mul(w, abc[1][i]));
-    if (i < rv.nb_public) {
+    if (vk_mask ? vk_mask[i] != 0 : i < rv.nb_public) {
       Fe<Fr> k = add(add(mul(tw.beta, abc[0][i]), mul(tw.alpha, abc[1][i])), abc[2][i]);
       spub = add(spub, mul(w, k));
     }
@@ -747,6 +753,27 @@ int o_g16_prove(int curve, const size_t* sizes, uint8_t* const* g1, uint8_t* con
     pk.infA = inf[0];
     pk.infB = inf[1];
     return g16_prove<C>(pk, nb_public, wires, a, b, c, nc, r, s, nthreads, ar, bs, krs);
+  };
+  if (curve == 0) return run(BN{});
+  if (curve == 1) return run(BLS{});
+  return -1;
+}
+
+int o_g16_check_mask(int curve, size_t nc, size_t nb_wires, size_t nb_public, const uint32_t* const* rp,
+                     const uint32_t* const* wire, const uint8_t* const* coeff, const uint8_t* toxic,
+                     const uint8_t* wires, const uint8_t* r, const uint8_t* s, const uint8_t* ar,
+                     const uint8_t* bs, const uint8_t* krs, const uint8_t* vk_mask) {
+  R1csView rv = make_r1cs(nc, nb_wires, nb_public, rp, wire, coeff);
+  auto run = [&](auto tag) {
+    using C = decltype(tag);
+    using Fr = typename C::Fr;
+    Toxic<C> tw;
+    tw.t = load_fe<Fr>(toxic);
+    tw.alpha = load_fe<Fr>(toxic + 32);
+    tw.beta = load_fe<Fr>(toxic + 64);
+    tw.gamma = load_fe<Fr>(toxic + 96);
+    tw.delta = load_fe<Fr>(toxic + 128);
+    return g16_check<C>(rv, tw, wires, r, s, ar, bs, krs, vk_mask);
   };
   if (curve == 0) return run(BN{});
   if (curve == 1) return run(BLS{});

@@ -530,3 +530,95 @@ def g16_prove(c: CurveParams, pk, wires, a, b, cc, r_: int, s_: int):
     krs = G1.add(krs, G1.mul(bs1, r_) if bs1 else None)
     bs = G2.add(G2.add(G2.msm(wB, pk["g2_B"]), G2.mul(pk["g2_delta"], s_)), pk["g2_beta"])
     return ar, bs, krs
+
+
+# ----------------------------------------------------------------------------
+# BSB22 commitments (prove.go:82-139; verify.go:86-121; constraint/commitment.go)
+#
+# The arithmetic lives in gnark-crypto (not vendored): pedersen.ProvingKey
+# {Basis, BasisExpSigma} with Commit = MultiExp(Basis, v) and ProveKnowledge =
+# MultiExp(BasisExpSigma, v); G1Affine.Fold(points, c) = sum_i c^i points[i];
+# fr.Hash(msg, dst, count) = RFC 9380 hash_to_field: expand_message_xmd with
+# SHA-256, L = 16 + ceil(Bits / 8) = 48 bytes per element, big-endian mod r;
+# hash_to_field.New(dst) is the hash.Hash whose Sum is fr.Hash(msg, dst, 1)[0]
+# as 32 big-endian bytes; G1Affine.Marshal is the UNCOMPRESSED encoding
+# (verify.go:88 sizes its buffer with SizeOfG1AffineUncompressed).  Pinned by
+# RFC 9380's expand_message_xmd test vectors (tests/test_oracle.py) and by the
+# exponent-form verification of whole proofs (verify.go's pairing equation +
+# pedersen.BatchVerifyMultiVk, restated for a setup whose toxic waste is known).
+# ----------------------------------------------------------------------------
+COMMITMENT_DST = b"bsb22-commitment"  # constraint.CommitmentDst (constraint/commitment.go:7)
+POK_DST = b"G16-BSB22"                # prove.go:133, verify.go:110
+
+
+def expand_message_xmd(msg: bytes, dst: bytes, len_in_bytes: int) -> bytes:
+    """RFC 9380 section 5.3.1 with H = SHA-256 (b_in_bytes 32, s_in_bytes 64)."""
+    import hashlib
+    ell = (len_in_bytes + 31) // 32
+    assert ell <= 255 and len(dst) <= 255 and len_in_bytes < 65536
+    dst_prime = dst + bytes([len(dst)])
+    msg_prime = bytes(64) + msg + len_in_bytes.to_bytes(2, "big") + b"\x00" + dst_prime
+    b0 = hashlib.sha256(msg_prime).digest()
+    bi = hashlib.sha256(b0 + b"\x01" + dst_prime).digest()
+    out = bi
+    for i in range(2, ell + 1):
+        bi = hashlib.sha256(bytes(x ^ y for x, y in zip(b0, bi)) + bytes([i]) + dst_prime).digest()
+        out += bi
+    return out[:len_in_bytes]
+
+
+def fr_byte_len(c: CurveParams) -> int:
+    """(fr.Bits - 1) / 8 + 1 (prove.go:98)."""
+    return (c.r.bit_length() - 1) // 8 + 1
+
+
+def hash_to_fr(c: CurveParams, msg: bytes, dst: bytes, count: int = 1):
+    """gnark-crypto fr.Hash: count elements of RFC 9380 hash_to_field."""
+    L = 16 + fr_byte_len(c)
+    u = expand_message_xmd(msg, dst, count * L)
+    return [int.from_bytes(u[i * L:(i + 1) * L], "big") % c.r for i in range(count)]
+
+
+def marshal_fr(c: CurveParams, x: int) -> bytes:
+    """fr.Element.Marshal: canonical value, big-endian."""
+    return (x % c.r).to_bytes(fr_byte_len(c), "big")
+
+
+def marshal_g1(c: CurveParams, P) -> bytes:
+    """G1Affine.Marshal (RawBytes, uncompressed): X || Y big-endian; infinity is
+    all zero with the uncompressed-infinity flag where the curve has one
+    (BLS12-377: 0b010 << 5 in the top byte; BN254: none)."""
+    n = 8 * c.fp_limbs
+    if P is None:
+        out = bytearray(2 * n)
+        if c.name != "bn254":
+            out[0] = 0b010 << 5
+        return bytes(out)
+    return P[0].to_bytes(n, "big") + P[1].to_bytes(n, "big")
+
+
+def serialize_commitment(private_commitment: bytes, public_committed, field_byte_len: int) -> bytes:
+    """constraint.SerializeCommitment (constraint/commitment.go:70-82)."""
+    return private_commitment + b"".join(int(v).to_bytes(field_byte_len, "big") for v in public_committed)
+
+
+def bsb22_commitment_value(c: CurveParams, D, hashed_values) -> int:
+    """The commitment wire's value from the overridden BSB22 hint (prove.go:83-108):
+    hash_to_field(Marshal(D) || public/commitment-committed values)."""
+    msg = serialize_commitment(marshal_g1(c, D), [v % c.r for v in hashed_values], fr_byte_len(c))
+    return hash_to_fr(c, msg, COMMITMENT_DST, 1)[0]
+
+
+def pok_challenge(c: CurveParams, commitment_wire_values) -> int:
+    """prove.go:129-136: fr.Hash(concat Marshal(w[CommitmentIndex_i]), "G16-BSB22", 1)[0]."""
+    return hash_to_fr(c, b"".join(marshal_fr(c, v) for v in commitment_wire_values), POK_DST, 1)[0]
+
+
+def fold_points(c: CurveParams, points, coeff: int):
+    """G1Affine.Fold (prove.go:137): sum_i coeff^i points[i]."""
+    G = Group(c, False)
+    acc, e = None, 1
+    for P in points:
+        acc = G.add(acc, G.mul(P, e) if P else None)
+        e = e * coeff % c.r
+    return acc

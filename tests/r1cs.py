@@ -150,3 +150,59 @@ def squaring_chain_fast(k: int, curve: str = "bn254", x: int = 2):
     b = np.concatenate([Wa[2:2 + k], Wa[2 + k:3 + k]]).tobytes()
     cc = np.concatenate([Wa[3:3 + k], Wa[1:2]]).tobytes()
     return r1, W, a, b, cc
+
+
+def commitment_chain(k: int, curve: str = "bn254", ncommit: int = 1, x: int = 3):
+    """squaring_chain(k) plus `ncommit` BSB22 commitments, the shape frontend
+    api.Commit compiles to (the Bsb22CommitmentComputePlaceholder hint whose
+    output wire is the commitment, prove.go:82-109; commitment info as in
+    constraint/commitment.go:9-14):
+
+      wires: 0 ONE, 1 Y (public), 2 X (secret), 3..2+k chain, then per
+             commitment i: cm_i (commitment wire), u_i (internal)
+      commitment i commits to private chain wires {2+i, 5+i, 8+i, ...} (every
+             third wire, disjoint across commitments) and to the public Y; for
+             i > 0 also to cm_{i-1} (a commitment-committed wire)
+      constraints: the chain, AssertIsEqual(w_k, Y), and u_i = cm_i * v with
+             v = X (i = 0) or u_{i-1}.
+
+    Returns (r1, info, solve): solve(hint) fills W, calling
+    hint(i, hashed_values, committed_values) -> commitment value (the
+    overridden hint; `hashed` = PublicAndCommitmentCommitted values)."""
+    assert k >= 3 * ncommit + 6
+    nb_public = 2
+    base = 3 + k
+    cm = [base + 2 * i for i in range(ncommit)]
+    u = [base + 2 * i + 1 for i in range(ncommit)]
+    cons = []
+    for j in range(k):
+        wj = 2 + j
+        cons.append(([(wj, 1)], [(wj, 1)], [(wj + 1, 1)]))
+    cons.append(([(0, 1)], [(2 + k, 1)], [(1, 1)]))
+    info = []
+    for i in range(ncommit):
+        priv = list(range(2 + i, 3 + k, 3 * ncommit))[:12]
+        pac = [1] + ([cm[i - 1]] if i > 0 else [])
+        info.append({"public_and_commitment_committed": pac, "nb_public_committed": 1,
+                     "private_committed": sorted(priv), "commitment_index": cm[i]})
+        v = 2 if i == 0 else u[i - 1]
+        cons.append(([(cm[i], 1)], [(v, 1)], [(u[i], 1)]))
+    r1 = R1CS(curve, nb_public=nb_public, nb_wires=base + 2 * ncommit, constraints=cons)
+    r = pyref.CURVES[curve].r
+
+    def solve(hint):
+        W = [1, 0, x % r] + [0] * (k + 2 * ncommit)
+        v = x % r
+        for j in range(k):
+            v = v * v % r
+            W[3 + j] = v
+        W[1] = v
+        for i, ci in enumerate(info):
+            hashed = [W[w] for w in ci["public_and_commitment_committed"]]
+            W[cm[i]] = hint(i, hashed, [W[w] for w in ci["private_committed"]]) % r
+            prev = W[2] if i == 0 else W[u[i - 1]]
+            W[u[i]] = W[cm[i]] * prev % r
+        assert r1.is_satisfied(W)
+        return W
+
+    return r1, info, solve

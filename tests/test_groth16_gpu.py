@@ -175,3 +175,61 @@ def test_groth16_multi_contexts_small(gm_ctx, oracle, cname, k, ndev):
             mpk.free()
     assert got == exp
     assert oracle.g16_check(cname, r1, tox, enc(W), rb, sb, *got) == 7
+
+
+@pytest.mark.parametrize("cname,ncommit,precompute", [("bn254", 1, False), ("bn254", 2, True),
+                                                      ("bls12377", 2, False)])
+def test_groth16_bsb22_commitments(gm_ctx, oracle, cname, ncommit, precompute):
+    """A circuit with one / two BSB22 commitments (prove.go:82-139) at n = 2^13:
+    the oracle solves it through the overridden commitment hint, proves and is
+    verified in the exponent; the device side gets the K filter exactly as
+    kWires() computes it (integration/go/icicle_bn254/icicle.go; prove.go:243-245)
+    and the Pedersen commitments, proofs of knowledge and the fold run as device
+    MSMs (gm_msm; pedersen Commit / ProveKnowledge are MultiExps).  Every proof
+    element must equal the oracle's byte for byte."""
+    import numpy as np
+    import gnark_mi355x as gm
+    c = pyref.CURVES[cname]
+    r1, info, solve = R.commitment_chain(4100, cname, ncommit)
+    assert r1.domain_size == 1 << 13
+    tox = [t % c.r for t in TOXIC]
+    sig = [0x5151515151 + 7 * i for i in range(ncommit)]
+    pk = oracle.g16_setup_bsb22(cname, r1, info, tox, sig)
+    exp = oracle.g16_prove_bsb22(cname, pk, r1, info, solve, 0x1357, 0x2468)
+    assert oracle.bsb22_check(cname, r1, pk, info, exp, sig)
+    # K filter of the Go hook (kWires): private wires minus committed and commitment wires
+    drop = set(w for ci in info for w in ci["private_committed"]) | set(ci["commitment_index"] for ci in info)
+    kw = [w for w in range(r1.nb_public, r1.nb_wires) if w not in drop]
+    assert kw == pk["k_wires"]
+    dpk = gm.ProvingKey(gm_ctx, cname, dict(pk, k_wires=kw), r1.domain_size, r1.nb_wires, r1.nb_public,
+                        precompute=precompute)
+    try:
+        got = dpk.prove(exp["Wb"], exp["a"], exp["b"], exp["c"], exp["rb"], exp["sb"])
+    finally:
+        dpk.free()
+    assert got == (exp["ar"], exp["bs"], exp["krs"])
+    # Pedersen side on the device
+    W = exp["W"]
+    enc = lambda vals: R.encode_vec(cname, vals)
+    g1b = gm.point_bytes(cname, False)
+    poks = b""
+    for i, ci in enumerate(info):
+        vals = enc([W[w] for w in ci["private_committed"]])
+        m = len(ci["private_committed"])
+        S = gm_ctx.copy_to_device(vals)
+        for key, want in (("basis", exp["commitments"][i]), ("basis_sigma", None)):
+            P = gm_ctx.copy_to_device(pk["ck"][i][key])
+            aff = gm_ctx.msm(cname, S, P, m)[1]
+            P.free()
+            if want is not None:
+                assert aff == want, ("commitment", i)
+            else:
+                poks += aff
+        S.free()
+    chal = pyref.pok_challenge(c, [W[ci["commitment_index"]] for ci in info])
+    S = gm_ctx.copy_to_device(enc([pow(chal, i, c.r) for i in range(ncommit)]))
+    P = gm_ctx.copy_to_device(poks)
+    assert gm_ctx.msm(cname, S, P, ncommit)[1] == exp["pok"]
+    S.free()
+    P.free()
+    assert len(poks) == ncommit * g1b

@@ -434,6 +434,106 @@ def test_msm_async_pipelined(gm_ctx, oracle):
             c[4].free()
 
 
+def test_msm_async_interleaved_with_sync(gm_ctx, oracle):
+    """Synchronous MSMs (small and large: a large one also takes a readback
+    buffer for its max-span check) issued while two async MSMs are pending must
+    not reuse the pending MSMs' pinned readback buffers (gnark_mi355x.h: each
+    pending MSM keeps its own until gm_msm_wait)."""
+    import gnark_mi355x as gm
+    sizes = [(3000, False), (1 << 18, False), (700, True), (5000, False), (1 << 18, False), (900, True)]
+    data = []
+    for k, (n, g2) in enumerate(sizes):
+        S = gm_ctx.random_scalars("bn254", n, seed=0xC0 + k)
+        K = gm_ctx.random_scalars("bn254", n, seed=0xD0 + k)
+        P = gm_ctx.batch_mul_base("bn254", g2, gm.generator("bn254", g2), K, n)
+        K.free()
+        data.append((n, g2, S, P, oracle.msm("bn254", g2, S.to_host(), P.to_host())))
+    try:
+        a = gm_ctx.msm_async("bn254", data[0][2], data[0][3], data[0][0], data[0][1])
+        b = gm_ctx.msm_async("bn254", data[2][2], data[2][3], data[2][0], data[2][1])
+        for n, g2, S, P, exp in data[1:] + data[1:]:  # 10 synchronous MSMs in between
+            assert gm_ctx.msm("bn254", S, P, n, g2)[1] == exp
+        assert a.wait()[1] == data[0][4]
+        assert b.wait()[1] == data[2][4]
+    finally:
+        for d in data:
+            d[2].free()
+            d[3].free()
+
+
+def _glv_bls12377():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "glv_constants", os.path.join(os.path.dirname(__file__), "..", "tools", "glv_constants.py"))
+    glv = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(glv)
+    return glv.derive_bls12377()
+
+
+@pytest.mark.parametrize("g2,window", [(False, 0), (False, 13), (True, 0), (True, 16)])
+def test_msm_glv_bls12377_split_boundaries(gm_ctx, oracle, g2, window):
+    """BLS12-377 GLV (msm_impl.hpp GlvBls377: k2 = floor(k / lambda), k1 = k mod
+    lambda, lambda = x^2 - 1; phi = (beta x, y), beta^2 on the G2 twist): scalars
+    at the division's edges against the oracle's unsplit Pippenger, with the
+    split on and off."""
+    c = pyref.CURVES["bls12377"]
+    d = _glv_bls12377()
+    r, lam = c.r, d["lam"]
+    special = [0, 1, 2, r - 1, r - 2, lam, lam - 1, lam + 1, lam * lam, lam * lam - 1, lam * lam + lam,
+               lam * lam + lam - 1, r - lam, (r - 1) // 2, 1 << 252, (1 << 127) - 1, 1 << 127, 2 * lam]
+    n = 2048 + 21 if not g2 else 512 + 21
+    pbytes = 192 if g2 else 96
+    sc = pyref.random_scalars(c, n, 0x71F + g2)
+    sc[:len(special)] = special
+    sb = b"".join(pyref.encode_fr(c, s) for s in sc)
+    pb = _random_points_host(gm_ctx, "bls12377", g2, n, 0x720 + g2)
+    pb = pyref.encode_point(c, None, g2) + pb[pbytes:]  # an infinity point
+    S = gm_ctx.copy_to_device(sb)
+    P = gm_ctx.copy_to_device(pb)
+    exp = oracle.msm("bls12377", g2, sb, pb)
+    try:
+        gm_ctx.set_msm_window(window)
+        for glv in (1, 0):
+            gm_ctx.set_msm_glv(glv)
+            for m in (1, 9, 64, n):
+                exp_m = exp if m == n else oracle.msm("bls12377", g2, sb[:32 * m], pb[:pbytes * m])
+                assert gm_ctx.msm("bls12377", S, P, m, g2)[1] == exp_m, (g2, window, glv, m)
+    finally:
+        gm_ctx.set_msm_window(0)
+        gm_ctx.set_msm_glv(-1)
+        S.free()
+        P.free()
+
+
+@pytest.mark.parametrize("glv", [1, 0])
+def test_msm_bn254_g1_2p20_bench_input_vs_oracle(gm_ctx, oracle, glv):
+    """BASELINE configs[1] at full size, exactly the bench's input (bench.py:
+    uniform scalars seed 0x5EED0002, points [k_i]G1 seed 0x5EED1002, plus the
+    edge set -- 1% infinity points, a 1% run of equal points, scalars 0, 1, r-1),
+    GLV split on (the default path) and off, against the oracle's Pippenger."""
+    import importlib.util
+    import gnark_mi355x as gm
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(os.path.dirname(__file__), "..", "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    n = 1 << 20
+    S = gm_ctx.random_scalars("bn254", n, 0x5EED0002)
+    K = gm_ctx.random_scalars("bn254", n, 0x5EED1002)
+    P = gm_ctx.batch_mul_base("bn254", False, gm.generator("bn254"), K, n)
+    K.free()
+    try:
+        bench.add_edge_set(gm_ctx, gm, S, P, n)
+        exp = oracle.msm("bn254", False, S.to_host(), P.to_host())
+        gm_ctx.set_msm_glv(glv)
+        assert gm_ctx.msm("bn254", S, P, n)[1] == exp
+        pend = [gm_ctx.msm_async("bn254", S, P, n) for _ in range(2)]  # the bench's pipelined form
+        assert [q.wait()[1] for q in pend] == [exp, exp]
+    finally:
+        gm_ctx.set_msm_glv(-1)
+        S.free()
+        P.free()
+
+
 @pytest.mark.parametrize("g2,window", [(False, 0), (False, 11), (False, 16), (True, 0), (True, 16)])
 def test_msm_glv_split_boundaries(gm_ctx, oracle, g2, window):
     """BN254 G1 / G2 MSMs from gnark-layout points run the GLV split (k = k1 + k2

@@ -157,3 +157,61 @@ def test_oracle_groth16_random_circuit(oracle, cname):
     rb, sb = enc([3]), enc([4])
     proof = oracle.g16_prove(cname, pk, r1.nb_public, enc(W), enc(a), enc(b), enc(cc), rb, sb)
     assert oracle.g16_check(cname, r1, tox, enc(W), rb, sb, *proof) == 7
+
+
+# ---- BSB22 commitments (prove.go:82-139) --------------------------------------
+
+def test_expand_message_xmd_rfc9380_vectors():
+    """RFC 9380 appendix K.1 (expand_message_xmd, SHA-256,
+    DST "QUUX-V01-CS02-with-expander-SHA256-128"): the published algorithm
+    gnark-crypto's fr.Hash / hash_to_field.New build on."""
+    dst = b"QUUX-V01-CS02-with-expander-SHA256-128"
+    assert pyref.expand_message_xmd(b"", dst, 0x20).hex() == \
+        "68a985b87eb6b46952128911f2a4412bbc302a9d759667f87f7a21d803f07235"
+    assert pyref.expand_message_xmd(b"abc", dst, 0x20).hex() == \
+        "d8ccab23b5985ccea865c6c97b6e5b8350e794e603b4b97902f53a8a0d605615"
+    assert pyref.expand_message_xmd(b"", dst, 0x80).hex().startswith(
+        "af84c27ccfd45d41914fdff5df25293e221afc53d8ad2ac06d5e3e29485dadbe")
+
+
+def test_bsb22_serialization_shapes():
+    """SerializeCommitment (constraint/commitment.go:70-82) = Marshal(D) (the
+    uncompressed point, verify.go:88) || each committed public value as
+    (fr.Bits-1)/8+1 big-endian bytes; fr.Hash takes 16 + 32 = 48 bytes per element."""
+    for cname in ("bn254", "bls12377"):
+        c = pyref.CURVES[cname]
+        G = pyref.Group(c, False)
+        D = G.mul(G.generator(), 12345)
+        s = pyref.serialize_commitment(pyref.marshal_g1(c, D), [7, c.r - 1], pyref.fr_byte_len(c))
+        assert len(s) == 2 * 8 * c.fp_limbs + 2 * 32
+        assert s[-32:] == (c.r - 1).to_bytes(32, "big")
+        assert pyref.marshal_g1(c, D)[:8 * c.fp_limbs] == D[0].to_bytes(8 * c.fp_limbs, "big")
+        v = pyref.hash_to_fr(c, b"msg", pyref.COMMITMENT_DST, 2)
+        assert len(v) == 2 and all(0 <= x < c.r for x in v) and v[0] != v[1]
+
+
+@pytest.mark.parametrize("cname,ncommit", [("bn254", 1), ("bn254", 2), ("bls12377", 2)])
+def test_oracle_groth16_bsb22_verifies(oracle, cname, ncommit):
+    """The oracle's prover with BSB22 commitments (hint override, Pedersen
+    commit / proof of knowledge, fold, K filter) produces proofs that satisfy
+    verify.go's equation (exponent form, with the commitment wires and the
+    private committed wires on the verifier's side) and the folded PoK
+    statement; a wrong PoK or a missing K filter is rejected."""
+    r1, info, solve = R.commitment_chain(40, cname, ncommit)
+    tox = [0x1234567 + i * 0x99999 for i in range(5)]
+    sig = [0xABCDEF + 17 * i for i in range(ncommit)]
+    pk = oracle.g16_setup_bsb22(cname, r1, info, tox, sig)
+    pr = oracle.g16_prove_bsb22(cname, pk, r1, info, solve, 0x1111, 0x2222)
+    assert oracle.bsb22_check(cname, r1, pk, info, pr, sig)
+    c = pyref.CURVES[cname]
+    bad = dict(pr)
+    bad["pok"] = pyref.encode_point(c, pyref.Group(c, False).generator(), False)
+    assert not oracle.bsb22_check(cname, r1, pk, info, bad, sig)
+    # the same witness proved WITHOUT the K filter double-counts the committed wires
+    full = dict(pk)
+    full["g1_K"] = pk["g1_K_full"]
+    full["sizes"] = pk["sizes"].copy()
+    full["sizes"][4] = r1.nb_wires - r1.nb_public
+    ar, bs, krs = oracle.g16_prove(cname, full, r1.nb_public, pr["Wb"], pr["a"], pr["b"], pr["c"], pr["rb"], pr["sb"])
+    nf = dict(pr, ar=ar, bs=bs, krs=krs)
+    assert not oracle.bsb22_check(cname, r1, pk, info, nf, sig)

@@ -154,3 +154,60 @@ def test_staged_inputs_by_level(gm_ctx, oracle, cname, k):
     finally:
         st.free()
         dpk.free()
+
+
+def test_pk_cache_rejects_corrupt_headers_and_indices(gm_ctx, oracle, tmp_path):
+    """gm_g16_pk_load_cache checks the header invariants, the device-layout
+    fingerprint and every compaction index against the wire slice (k_gather_fr
+    reads wires[idx] unchecked), instead of reading a stale / corrupt cache."""
+    import struct
+    import gnark_mi355x as gm
+    r1, pk, (W, A, B, C), rb, sb, exp = _setup(oracle, "bn254", 300)
+    dpk = gm.ProvingKey(gm_ctx, "bn254", pk, r1.domain_size, r1.nb_wires, r1.nb_public)
+    path = str(tmp_path / "pk.cache")
+    try:
+        dpk.save_cache(path)
+        _corrupt_cache_cases(gm_ctx, gm, dpk, path, r1, (W, A, B, C), rb, sb, exp)
+    finally:
+        dpk.free()
+
+
+def _corrupt_cache_cases(gm_ctx, gm, dpk, path, r1, inputs, rb, sb, exp):
+    import struct
+    W, A, B, C = inputs
+    good = open(path, "rb").read()
+    HDR = 176  # CacheHeader (pk_io.hip)
+    off_n, off_layout, off_wires = 24, 16, 32
+
+    def load_with(blob, match):
+        with open(path, "wb") as f:
+            f.write(blob)
+        with pytest.raises(gm.GmError, match=match):
+            gm.ProvingKey.from_cache(gm_ctx, path)
+
+    b = bytearray(good)
+    b[off_n:off_n + 8] = struct.pack("<Q", r1.domain_size + 1)
+    load_with(bytes(b), "domain size")
+    b = bytearray(good)
+    b[off_layout:off_layout + 4] = struct.pack("<I", 0xDEAD)
+    load_with(bytes(b), "layout")
+    b = bytearray(good)
+    b[off_wires:off_wires + 8] = struct.pack("<Q", 0)
+    load_with(bytes(b), "wire counts")
+    # walk to the first compaction map (array 5) and point one entry past the wires
+    pos = HDR + 3 * 64 + 2 * 128
+    for _ in range(5):
+        (sz,) = struct.unpack_from("<Q", good, pos)
+        pos += 8 + sz
+    (sz,) = struct.unpack_from("<Q", good, pos)
+    assert sz > 0
+    b = bytearray(good)
+    b[pos + 8:pos + 12] = struct.pack("<I", r1.nb_wires)
+    load_with(bytes(b), "compaction index")
+    with open(path, "wb") as f:
+        f.write(good)
+    back = gm.ProvingKey.from_cache(gm_ctx, path, like=dpk)
+    try:
+        assert back.prove(W, A, B, C, rb, sb) == exp
+    finally:
+        back.free()
