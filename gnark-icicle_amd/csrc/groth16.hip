@@ -42,6 +42,21 @@ int check_curve_id(int curve) {
 }
 
 namespace {
+// Entries of the shared wire plan -> entries of array X: value w * sin + i
+// (wire i of window copy w; sin = 0 for plain layouts) becomes
+// w * sout + map[i], or MSM_SKIP when X has no point for wire i.
+__global__ void k_map_plan_vals(const uint32_t* __restrict__ vals, const uint32_t* __restrict__ offsets,
+                                uint32_t total, size_t M, const uint32_t* __restrict__ map, uint32_t sin,
+                                uint32_t sout, uint32_t* __restrict__ out) {
+  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= M || j >= offsets[total]) return;
+  const uint32_t v = vals[j];
+  const uint32_t raw = v & 0x7fffffffu;
+  const uint32_t w = sin ? raw / sin : 0u;
+  const uint32_t m = map[raw - w * sin];
+  out[j] = (m == MSM_SKIP ? MSM_SKIP : w * sout + m) | (v & 0x80000000u);
+}
+
 // dst[i] = src[idx[i]] (Fr, 32 bytes) -- device-side scalar compaction
 __global__ void k_gather_fr(const uint4* __restrict__ src, const uint32_t* __restrict__ idx, size_t n,
                             uint4* __restrict__ dst) {
@@ -79,9 +94,77 @@ size_t internal_point_bytes(int curve, bool g2) {
 }
 
 void pk_release(gm_g16_pk* pk) {
-  for (void* q : {pk->A, pk->B, pk->Z, pk->K, pk->B2, pk->idxA, pk->idxB, pk->idxK})
+  for (void* q : {pk->A, pk->B, pk->Z, pk->K, pk->B2, pk->idxA, pk->idxB, pk->idxK, pk->wmap[0], pk->wmap[1],
+                  pk->wmap[2]})
     if (q) hipFree(q);
   delete pk;
+}
+
+void wire_plan_choice(size_t span, size_t nbA, size_t nbB, size_t nbK, bool out[3]) {
+  const char* env = getenv("GM_G16_WIRE_PLAN");  // read per key (tests flip it)
+  const bool on = !env || atoi(env) != 0;
+  const size_t cnt[3] = {nbA, nbB, nbK};
+  int k = 0;
+  for (int x = 0; x < 3; x++) {
+    out[x] = on && span > 0 && cnt[x] <= span && 32 * cnt[x] >= 31 * span;
+    k += out[x];
+  }
+  if (k < 2)
+    for (int x = 0; x < 3; x++) out[x] = false;
+}
+
+int pk_setup_wire_plan(gm_ctx* ctx, gm_g16_pk* pk, const uint32_t* ia, const uint32_t* ib, const uint32_t* ik) {
+  const size_t span = pk->whi - pk->wlo;
+  bool want[3];
+  wire_plan_choice(span, pk->nbA, pk->nbB, pk->nbK, want);
+  const int frbits = pk->curve == GM_BN254 ? CurveBN254::FR_BITS : CurveBLS12377::FR_BITS;
+  MsmPrecomp pw;
+  if (pk->precomp) {
+    pw = msm_choose_precomp(span, frbits);
+    pw.stride = span;
+  }
+  const uint32_t* idx[3] = {ia, ib, ik};
+  const size_t cnt[3] = {pk->nbA, pk->nbB, pk->nbK};
+  const MsmPrecomp* pre[3] = {&pk->preA, &pk->preB, &pk->preK};
+  std::vector<uint32_t> map[3];
+  bool ident[3] = {false, false, false};
+  int k = 0;
+  for (int x = 0; x < 3; x++) {
+    if (!want[x]) continue;
+    // a precomputed array must have the plan's window geometry
+    if (pk->precomp && (pre[x]->c != pw.c || pre[x]->W != pw.W || pre[x]->narrow != pw.narrow)) {
+      want[x] = false;
+      continue;
+    }
+    map[x].assign(span, MSM_SKIP);
+    bool ok = true;
+    for (size_t j = 0; j < cnt[x] && ok; j++) {
+      const uint32_t w = idx[x][j];
+      if (w >= span || map[x][w] != MSM_SKIP) ok = false;  // a wire used twice: own plan
+      else map[x][w] = (uint32_t)j;
+    }
+    if (!ok) {
+      want[x] = false;
+      continue;
+    }
+    ident[x] = cnt[x] == span;
+    for (size_t i = 0; i < span && ident[x]; i++) ident[x] = map[x][i] == i;
+    k++;
+  }
+  if (k < 2) return GM_OK;  // not worth a shared plan
+  for (int x = 0; x < 3; x++) {
+    if (!want[x]) continue;
+    pk->wshare[x] = true;
+    if (ident[x]) continue;
+    if (hipMalloc(&pk->wmap[x], 4 * span) != hipSuccess) {
+      set_error("pk upload: hipMalloc of the wire map failed");
+      return GM_ERR_OOM;
+    }
+    GM_HIP(hipMemcpy(pk->wmap[x], map[x].data(), 4 * span, hipMemcpyHostToDevice));
+  }
+  pk->preW = pw;
+  (void)ctx;
+  return GM_OK;
 }
 
 int prepare_points_into(gm_ctx* ctx, int curve, bool g2, const void* gnark_dev, size_t count,
@@ -118,17 +201,66 @@ int pk_upload_ranges(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsigned f
   pk->nbZ = rg.hiZ - rg.loZ;
   pk->precomp = (flags & GM_PK_PRECOMPUTE) != 0;
   const int frbits = curve == GM_BN254 ? CurveBN254::FR_BITS : CurveBLS12377::FR_BITS;
-  if (pk->precomp) {
-    pk->preA = msm_choose_precomp(pk->nbA, frbits);
-    pk->preB = msm_choose_precomp(pk->nbB, frbits);
-    pk->preZ = msm_choose_precomp(pk->nbZ, frbits);
-    pk->preK = msm_choose_precomp(pk->nbK, frbits);
-  }
-  const size_t g1b = 2 * fp_bytes(curve), g2b = 4 * fp_bytes(curve);
   auto fail = [&](int code) {
     pk_release(pk);
     return code;
   };
+  // compaction maps (prove.go:157-178: drop wire i when InfinityA[i] / InfinityB[i];
+  // K: the k_wires survivors of filterHeap, prove.go:243-245, or nb_public + i)
+  std::vector<uint32_t> ia, ib, ik;
+  for (size_t i = 0; i < pk->nb_wires; i++) {
+    if (!h->infA[i]) ia.push_back((uint32_t)i);
+    if (!h->infB[i]) ib.push_back((uint32_t)i);
+  }
+  for (size_t i = 0; i < h->nbK; i++) {
+    const size_t w = h->k_wires ? (size_t)h->k_wires[i] : pk->nb_public + i;
+    if (w >= pk->nb_wires || w < pk->nb_public) {
+      set_error("pk upload: K wire index out of range");
+      return fail(GM_ERR_INVALID);
+    }
+    ik.push_back((uint32_t)w);
+  }
+  if (ia.size() != h->nbA || ib.size() != h->nbB || pk->nb_public + h->nbK > pk->nb_wires) {
+    set_error("pk upload: infinity masks inconsistent with nbA/nbB/nbK");
+    return fail(GM_ERR_INVALID);
+  }
+  // wire range this key's slices read
+  pk->wlo = 0;
+  pk->whi = pk->nb_wires;
+  if (rg.rebase) {
+    size_t lo = SIZE_MAX, hi = 0;
+    auto span = [&](const std::vector<uint32_t>& v, size_t a, size_t b) {
+      for (size_t i = a; i < b; i++) {
+        lo = std::min(lo, (size_t)v[i]);
+        hi = std::max(hi, (size_t)v[i] + 1);
+      }
+    };
+    span(ia, rg.loA, rg.hiA);
+    span(ib, rg.loB, rg.hiB);
+    span(ik, rg.loK, rg.hiK);
+    if (hi <= lo) lo = hi = 0;
+    pk->wlo = lo;
+    pk->whi = hi;
+    for (auto* v : {&ia, &ib, &ik})
+      for (auto& x : *v) x -= (x >= lo ? (uint32_t)lo : x);  // entries outside the slice are never read
+  }
+  // window geometry: arrays that may share the wire plan take the plan's
+  // (chosen for the wire span), the others their own
+  bool wsh[3];
+  wire_plan_choice(pk->whi - pk->wlo, pk->nbA, pk->nbB, pk->nbK, wsh);
+  if (pk->precomp) {
+    const MsmPrecomp pw = msm_choose_precomp(pk->whi - pk->wlo, frbits);
+    auto geom = [&](size_t cnt, bool shared) {
+      MsmPrecomp p = shared ? pw : msm_choose_precomp(cnt, frbits);
+      p.stride = cnt;
+      return p;
+    };
+    pk->preA = geom(pk->nbA, wsh[0]);
+    pk->preB = geom(pk->nbB, wsh[1]);
+    pk->preK = geom(pk->nbK, wsh[2]);
+    pk->preZ = msm_choose_precomp(pk->nbZ, frbits);
+  }
+  const size_t g1b = 2 * fp_bytes(curve), g2b = 4 * fp_bytes(curve);
   auto up = [&](const void* src, size_t bytes, void** dst) -> int {
     hipError_t e = hipMalloc(dst, bytes ? bytes : 16);
     if (e != hipSuccess) {
@@ -172,48 +304,10 @@ int pk_upload_ranges(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsigned f
       (rc = up_pts(PK_K, h->g1_K, pk->nbK, false, pk->preK, &pk->K)) ||
       (rc = up_pts(PK_B2, h->g2_B, pk->nbB, true, pk->preB, &pk->B2)))
     return fail(rc);
-  // compaction maps (prove.go:157-178: drop wire i when InfinityA[i] / InfinityB[i];
-  // K: the k_wires survivors of filterHeap, prove.go:243-245, or nb_public + i)
-  std::vector<uint32_t> ia, ib, ik;
-  for (size_t i = 0; i < pk->nb_wires; i++) {
-    if (!h->infA[i]) ia.push_back((uint32_t)i);
-    if (!h->infB[i]) ib.push_back((uint32_t)i);
-  }
-  for (size_t i = 0; i < h->nbK; i++) {
-    const size_t w = h->k_wires ? (size_t)h->k_wires[i] : pk->nb_public + i;
-    if (w >= pk->nb_wires || w < pk->nb_public) {
-      set_error("pk upload: K wire index out of range");
-      return fail(GM_ERR_INVALID);
-    }
-    ik.push_back((uint32_t)w);
-  }
-  if (ia.size() != h->nbA || ib.size() != h->nbB || pk->nb_public + h->nbK > pk->nb_wires) {
-    set_error("pk upload: infinity masks inconsistent with nbA/nbB/nbK");
-    return fail(GM_ERR_INVALID);
-  }
-  // wire range this key's slices read
-  pk->wlo = 0;
-  pk->whi = pk->nb_wires;
-  if (rg.rebase) {
-    size_t lo = SIZE_MAX, hi = 0;
-    auto span = [&](const std::vector<uint32_t>& v, size_t a, size_t b) {
-      for (size_t i = a; i < b; i++) {
-        lo = std::min(lo, (size_t)v[i]);
-        hi = std::max(hi, (size_t)v[i] + 1);
-      }
-    };
-    span(ia, rg.loA, rg.hiA);
-    span(ib, rg.loB, rg.hiB);
-    span(ik, rg.loK, rg.hiK);
-    if (hi <= lo) lo = hi = 0;
-    pk->wlo = lo;
-    pk->whi = hi;
-    for (auto* v : {&ia, &ib, &ik})
-      for (auto& x : *v) x -= (x >= lo ? (uint32_t)lo : x);  // entries outside the slice are never read
-  }
   if ((rc = up(ia.data() + rg.loA, 4 * pk->nbA, &pk->idxA)) || (rc = up(ib.data() + rg.loB, 4 * pk->nbB, &pk->idxB)) ||
       (rc = up(ik.data() + rg.loK, 4 * pk->nbK, &pk->idxK)))
     return fail(rc);
+  if ((rc = pk_setup_wire_plan(ctx, pk, ia.data() + rg.loA, ib.data() + rg.loB, ik.data() + rg.loK))) return fail(rc);
   auto cp = [](std::vector<uint8_t>& v, const void* s, size_t b) {
     v.resize(b);
     memcpy(v.data(), s, b);
@@ -395,6 +489,205 @@ struct RemoteH : HSource {
   }
 };
 
+// ---------------------------------------------------------------------------
+// computeH split across the devices of a gm_multi (the a, b, c
+// INTT + coset-NTT chains are independent).  Device 1 runs b's chain (and c's
+// with two devices), device 2 c's; each sends its result into device 0's
+// buffer (xGMI peer copy) and signals a ChainDone.  Device 0 runs a's chain,
+// then -- once b and c have arrived -- the fused pointwise + coset INTT, and
+// distributes the h slices.  Every device also runs its MSM shards meanwhile.
+// ---------------------------------------------------------------------------
+struct ChainDone {
+  std::mutex mu;
+  std::condition_variable cv;
+  bool recorded = false;  // `ev` recorded after the peer copies (or failure)
+  int rc = GM_OK;
+  hipEvent_t ev = nullptr;  // on the producer's auxiliary stream
+  void signal(int r) {
+    std::lock_guard<std::mutex> lk(mu);
+    recorded = true;
+    rc = r;
+    cv.notify_all();
+  }
+  // 1 = arrived, 0 = not yet (non-blocking), < 0 = producer failed
+  int ready(bool block) {
+    std::unique_lock<std::mutex> lk(mu);
+    if (block) cv.wait(lk, [&] { return recorded; });
+    if (!recorded) return 0;
+    if (rc) {
+      set_error("computeH chain device failed");
+      return rc;
+    }
+    lk.unlock();
+    if (block) return hipEventSynchronize(ev) == hipSuccess ? 1 : GM_ERR_DEVICE;
+    const hipError_t q = hipEventQuery(ev);
+    return q == hipSuccess ? 1 : (q == hipErrorNotReady ? 0 : GM_ERR_DEVICE);
+  }
+};
+
+// runs `f` with the context's main stream replaced by its auxiliary stream
+template <class F>
+int on_aux(gm_ctx* ctx, F&& f) {
+  hipStream_t main = ctx->stream;
+  ctx->stream = ctx->aux;
+  int rc = f();
+  ctx->stream = main;
+  return rc;
+}
+
+// Producer side (devices 1, 2): h slice from device 0 like RemoteH, plus the
+// chains of the host vectors it was given.
+template <class C>
+struct ChainRemoteH : RemoteH {
+  gm_ctx* ctx;
+  int dev0;
+  size_t nc, n;
+  struct Job {
+    const void* host;  // solution.B / .C
+    void* local;       // on this device
+    void* dst;         // device 0's buffer
+    ChainDone* done;
+  };
+  std::vector<Job> jobs;
+  hipEvent_t copied = nullptr;
+  std::thread th;
+  std::atomic<bool> queued{false};
+  std::atomic<int> copy_rc{GM_OK};
+  bool launched = false;
+  ChainRemoteH(SharedH* s, const void* d, gm_ctx* c, int dev0_, size_t nc_, size_t n_)
+      : RemoteH(s, d), ctx(c), dev0(dev0_), nc(nc_), n(n_) {}
+  int start() {
+    GM_HIP(hipEventCreateWithFlags(&copied, hipEventDisableTiming));
+    th = std::thread([this] {
+      int r = hipSetDevice(ctx->device) == hipSuccess ? GM_OK : GM_ERR_DEVICE;
+      for (auto& j : jobs)
+        if (r == GM_OK && nc && hipMemcpyAsync(j.local, j.host, 32 * nc, hipMemcpyHostToDevice, ctx->copy) != hipSuccess)
+          r = GM_ERR_DEVICE;
+      if (r == GM_OK && hipEventRecord(copied, ctx->copy) != hipSuccess) r = GM_ERR_DEVICE;
+      copy_rc = r;
+      queued = true;
+    });
+    return GM_OK;
+  }
+  int launch(bool block) {
+    if (launched || (!block && !queued.load())) return GM_OK;
+    if (th.joinable()) th.join();
+    launched = true;
+    int rc = copy_rc;
+    if (rc == GM_OK)
+      rc = on_aux(ctx, [&]() -> int {
+        GM_HIP(hipStreamWaitEvent(ctx->stream, copied, 0));
+        for (auto& j : jobs) {
+          int r = compute_h_chain<C>(ctx, j.local, nc, n);
+          if (r) return r;
+          if (ctx->device == dev0)
+            GM_HIP(hipMemcpyAsync(j.dst, j.local, 32 * n, hipMemcpyDeviceToDevice, ctx->stream));
+          else
+            GM_HIP(hipMemcpyPeerAsync(j.dst, dev0, j.local, ctx->device, 32 * n, ctx->stream));
+        }
+        for (auto& j : jobs) GM_HIP(hipEventRecord(j.done->ev, ctx->stream));
+        return GM_OK;
+      });
+    for (auto& j : jobs) j.done->signal(rc);
+    if (rc) set_error("computeH chain: " + std::string(gm_last_error()));
+    return rc;
+  }
+  int poll() override { return launch(false); }
+  int z_scalars(const void** zs) override {
+    int rc;
+    if ((rc = launch(true))) return rc;
+    return RemoteH::z_scalars(zs);
+  }
+  ~ChainRemoteH() override {
+    if (th.joinable()) th.join();
+    if (!launched)
+      for (auto& j : jobs) j.done->signal(GM_ERR_DEVICE);  // never leave device 0 waiting
+    hipStreamSynchronize(ctx->copy);
+    hipStreamSynchronize(ctx->aux);
+    if (copied) hipEventDestroy(copied);
+  }
+};
+
+// Device 0 side: a's chain as soon as a is on the device, the fused tail once
+// b and c have arrived, then `after_h` (the h slices to the other devices).
+template <class C>
+struct SplitH : HSource {
+  gm_ctx* ctx;
+  gm_g16_pk* pk;
+  void *da, *db, *dc;
+  const void* ha;
+  size_t nc;
+  std::vector<ChainDone*> remote;
+  EventPair ev;  // a: a copied (copy stream), b: h ready (aux)
+  std::thread th;
+  std::atomic<bool> queued{false};
+  std::atomic<int> copy_rc{GM_OK};
+  int stage = 0;  // 0: nothing launched, 1: a's chain launched, 2: tail launched
+  std::function<int()> after_h;
+  SplitH(gm_ctx* x, gm_g16_pk* k, void* a_, void* b_, void* c_, const void* ha_, size_t n_)
+      : ctx(x), pk(k), da(a_), db(b_), dc(c_), ha(ha_), nc(n_) {}
+  int start() {
+    int rc;
+    if ((rc = ev.create())) return rc;
+    th = std::thread([this] {
+      int r = hipSetDevice(ctx->device) == hipSuccess ? GM_OK : GM_ERR_DEVICE;
+      if (r == GM_OK && nc && hipMemcpyAsync(da, ha, 32 * nc, hipMemcpyHostToDevice, ctx->copy) != hipSuccess)
+        r = GM_ERR_DEVICE;
+      if (r == GM_OK && hipEventRecord(ev.a, ctx->copy) != hipSuccess) r = GM_ERR_DEVICE;
+      copy_rc = r;
+      queued = true;
+    });
+    return GM_OK;
+  }
+  int advance(bool block) {
+    int rc;
+    if (stage == 0) {
+      if (!block && !queued.load()) return GM_OK;
+      if (th.joinable()) th.join();
+      if (copy_rc) {
+        set_error("staged a upload failed");
+        return copy_rc;
+      }
+      rc = on_aux(ctx, [&]() -> int {
+        GM_HIP(hipStreamWaitEvent(ctx->stream, ev.a, 0));
+        return compute_h_chain<C>(ctx, da, nc, pk->n);
+      });
+      if (rc) return rc;
+      stage = 1;
+    }
+    if (stage == 1) {
+      for (ChainDone* d : remote) {
+        const int r = d->ready(block);
+        if (r < 0) return r;
+        if (r == 0) return GM_OK;  // not yet: a later poll
+      }
+      rc = on_aux(ctx, [&]() -> int {
+        int r = compute_h_finish<C>(ctx, da, db, dc, pk->n);
+        if (r) return r;
+        GM_HIP(hipEventRecord(ev.b, ctx->stream));
+        return GM_OK;
+      });
+      if (rc) return rc;
+      stage = 2;
+      if (after_h && (rc = after_h())) return rc;
+    }
+    return GM_OK;
+  }
+  int poll() override { return advance(false); }
+  int z_scalars(const void** zs) override {
+    int rc;
+    if ((rc = advance(true))) return rc;
+    GM_HIP(hipStreamWaitEvent(ctx->stream, ev.b, 0));
+    *zs = (const char*)da + 32 * pk->zlo;
+    return GM_OK;
+  }
+  ~SplitH() override {
+    if (th.joinable()) th.join();
+    hipStreamSynchronize(ctx->copy);
+    hipStreamSynchronize(ctx->aux);
+  }
+};
+
 template <class C>
 struct G16Sums {
   typename C::HG1F A[3], B[3], K[3], Z[3];
@@ -409,28 +702,57 @@ int g16_sums_t(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, HSource& hs, G
   hipStream_t st = ctx->stream;
   int rc;
   Arena arena(ctx);
-  DevBuf wA, wB, wK;
-  if ((rc = wA.alloc(arena, 32 * (pk->nbA ? pk->nbA : 1))) || (rc = wB.alloc(arena, 32 * (pk->nbB ? pk->nbB : 1))) ||
-      (rc = wK.alloc(arena, 32 * (pk->nbK ? pk->nbK : 1))))
-    return rc;
-  {
-    // device-side scalar compaction (icicle.go:231-278 do this on the host + H2D)
-    ProfScope ps(ctx, "gather_scalars");
-    if (pk->nbA)
-      hipLaunchKernelGGL(k_gather_fr, dim3(blocks_for(pk->nbA, 256)), dim3(256), 0, st, (const uint4*)wires_dev,
-                         (const uint32_t*)pk->idxA, pk->nbA, (uint4*)wA.p);
-    if (pk->nbB)
-      hipLaunchKernelGGL(k_gather_fr, dim3(blocks_for(pk->nbB, 256)), dim3(256), 0, st, (const uint4*)wires_dev,
-                         (const uint32_t*)pk->idxB, pk->nbB, (uint4*)wB.p);
-    if (pk->nbK)
-      hipLaunchKernelGGL(k_gather_fr, dim3(blocks_for(pk->nbK, 256)), dim3(256), 0, st, (const uint4*)wires_dev,
-                         (const uint32_t*)pk->idxK, pk->nbK, (uint4*)wK.p);
-  }
-  GM_HIP(hipGetLastError());
   const MsmPrecomp* pA = pk->precomp ? &pk->preA : nullptr;
   const MsmPrecomp* pB = pk->precomp ? &pk->preB : nullptr;
   const MsmPrecomp* pK = pk->precomp ? &pk->preK : nullptr;
   const MsmPrecomp* pZ = pk->precomp ? &pk->preZ : nullptr;
+  const MsmPrecomp* pX[3] = {pA, pB, pK};
+  const size_t nX[3] = {pk->nbA, pk->nbB, pk->nbK};
+  const void* idxX[3] = {pk->idxA, pk->idxB, pk->idxK};
+  // Scalars of the arrays with their own plan: device-side compaction
+  // (icicle.go:231-278 do this on the host + H2D)
+  DevBuf wX[3];
+  {
+    ProfScope ps(ctx, "gather_scalars");
+    for (int x = 0; x < 3; x++) {
+      if (pk->wshare[x]) continue;
+      if ((rc = wX[x].alloc(arena, 32 * (nX[x] ? nX[x] : 1)))) return rc;
+      if (nX[x])
+        hipLaunchKernelGGL(k_gather_fr, dim3(blocks_for(nX[x], 256)), dim3(256), 0, st, (const uint4*)wires_dev,
+                           (const uint32_t*)idxX[x], nX[x], (uint4*)wX[x].p);
+    }
+  }
+  GM_HIP(hipGetLastError());
+  // The shared wire plan (pk_setup_wire_plan): ONE digit / sort plan over the
+  // wire slice serves the A, B, B2 and K MSMs of arrays that cover it; an array
+  // with a wire map reads the plan's entries translated to its own points.
+  MsmPlan planX[3];
+  bool have[3] = {false, false, false};
+  if (pk->wshare[0] || pk->wshare[1] || pk->wshare[2]) {
+    MsmPlan planW;
+    const MsmPrecomp* pW = pk->precomp ? &pk->preW : nullptr;
+    if ((rc = msm_plan<C>(ctx, arena, wires_dev, pk->whi - pk->wlo, pW, planW))) return rc;
+    for (int x = 0; x < 3; x++) {
+      if (!pk->wshare[x]) continue;
+      planX[x] = planW;
+      planX[x].npts = pX[x] ? (size_t)pX[x]->W * pX[x]->stride : nX[x];
+      have[x] = true;
+      if (!pk->wmap[x] || planW.n == 0) continue;
+      ProfScope ps(ctx, "map_plan_vals");
+      DevBuf mv;
+      if ((rc = mv.alloc(arena, sizeof(uint32_t) * planW.M))) return rc;
+      hipLaunchKernelGGL(k_map_plan_vals, dim3(blocks_for(planW.M, 256)), dim3(256), 0, st, planW.vals,
+                         planW.offsets, planW.total, planW.M, (const uint32_t*)pk->wmap[x],
+                         pW ? (uint32_t)pW->stride : 0u, pX[x] ? (uint32_t)pX[x]->stride : 0u, mv.as<uint32_t>());
+      GM_HIP(hipGetLastError());
+      planX[x].vals = mv.as<uint32_t>();
+    }
+  }
+  // launch array x's MSM into `slot`: on the shared plan, or plan + launch
+  auto launch_x = [&](int x, Arena& slot, void* pts, MsmTail& t) -> int {
+    if (have[x]) return msm_launch<C, false>(ctx, slot, planX[x], pts, t);
+    return msm_device_launch<C, false>(ctx, slot, wX[x].p, pts, nX[x], true, pX[x], t);
+  };
   // The five MSMs run pipelined two deep: the host tail of one (readback checks
   // and Horner, msm_finish) overlaps the device work of the next, each MSM in
   // one of the context's two slot arenas.  The G1 and G2 B-MSMs
@@ -438,19 +760,19 @@ int g16_sums_t(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, HSource& hs, G
   SlotArena s0(ctx), s1(ctx);
   MsmTail tA, tB, tB2, tK, tZ;
   if ((rc = hs.poll()) || (rc = s0.take())) return rc;
-  if ((rc = msm_device_launch<C, false>(ctx, *s0.a, wA.p, pk->A, pk->nbA, true, pA, tA))) return rc;
+  if ((rc = launch_x(0, *s0.a, pk->A, tA))) return rc;
   if ((rc = hs.poll()) || (rc = s1.take())) return rc;
-  MsmPlan planB;
-  if ((rc = msm_plan<C>(ctx, *s1.a, wB.p, pk->nbB, pB, planB)) ||
-      (rc = msm_launch<C, false>(ctx, *s1.a, planB, pk->B, tB)))
-    return rc;
+  if (!have[1]) {
+    if ((rc = msm_plan<C>(ctx, *s1.a, wX[1].p, pk->nbB, pB, planX[1]))) return rc;
+  }
+  if ((rc = msm_launch<C, false>(ctx, *s1.a, planX[1], pk->B, tB))) return rc;
   if ((rc = msm_finish<C, false>(ctx, tA, out.A))) return rc;
   s0.release();
-  if ((rc = hs.poll()) || (rc = msm_launch<C, true>(ctx, *s1.a, planB, pk->B2, tB2))) return rc;
+  if ((rc = hs.poll()) || (rc = msm_launch<C, true>(ctx, *s1.a, planX[1], pk->B2, tB2))) return rc;
   if ((rc = msm_finish<C, false>(ctx, tB, out.B))) return rc;
   if (on_ab) on_ab(out);
   if ((rc = hs.poll()) || (rc = s0.take())) return rc;
-  if ((rc = msm_device_launch<C, false>(ctx, *s0.a, wK.p, pk->K, pk->nbK, true, pK, tK))) return rc;
+  if ((rc = launch_x(2, *s0.a, pk->K, tK))) return rc;
   if ((rc = msm_finish<C, true>(ctx, tB2, out.B2))) return rc;
   s1.release();
   const void* zs = nullptr;
@@ -825,10 +1147,16 @@ int gm_g16_pk_upload_multi(gm_multi* m, int curve, const gm_g16_pk_host* h, unsi
   const int nd = (int)m->ctx.size();
   // device 0 also runs computeH (~19 ms at 2^24): it takes a smaller share of
   // the MSM work (GM_MULTI_SHARE0 = its weight relative to the others' 1.0)
+  // devices 0-2 also run computeH (split: one a / b / c chain each, device 0
+  // the tail and the h distribution; ~5 ms per chain, ~2.5 ms tail at 2^24):
+  // they take smaller MSM shares (GM_MULTI_SHARE0 / GM_MULTI_SHARE_H = weight
+  // relative to the others' 1.0)
   std::vector<double> w(nd, 1.0);
   if (nd > 1) {
     const char* s0 = getenv("GM_MULTI_SHARE0");
-    w[0] = s0 ? std::max(0.0, atof(s0)) : 0.6;
+    const char* sh = getenv("GM_MULTI_SHARE_H");
+    w[0] = s0 ? std::max(0.0, atof(s0)) : 0.7;
+    for (int d = 1; d < std::min(nd, 3); d++) w[d] = sh ? std::max(0.0, atof(sh)) : 0.85;
   }
   auto* mp = new gm_g16_pk_multi();
   mp->curve = curve;
@@ -918,6 +1246,33 @@ int g16_prove_multi_t(gm_multi* m, gm_g16_pk_multi* mp, const uint8_t* wires, co
       hz[d] = b.p;
     }
   }
+  // device 0's b / c buffers (peer-copy targets of the chains on devices 1, 2;
+  // one device: its own staged b, c)
+  void* d0bc[2] = {nullptr, nullptr};
+  const bool split = nd >= 2;
+  {
+    GM_HIP(hipSetDevice(m->ctx[0]->device));
+    DevBuf b, c;
+    const size_t n = mp->pk[0]->n;
+    if (int rc = b.alloc(*arenas[0], 32 * n)) return rc;
+    if (int rc = c.alloc(*arenas[0], 32 * n)) return rc;
+    d0bc[0] = b.p;
+    d0bc[1] = c.p;
+  }
+  // chain placement: b on device 1, c on device 2 (device 1 with two devices)
+  ChainDone chain_done[2];
+  const int chain_dev[2] = {split ? 1 : -1, nd >= 3 ? 2 : (split ? 1 : -1)};
+  for (int k = 0; k < 2 && split; k++) {
+    GM_HIP(hipSetDevice(m->ctx[chain_dev[k]]->device));
+    GM_HIP(hipEventCreateWithFlags(&chain_done[k].ev, hipEventDisableTiming));
+  }
+  struct EvFree {
+    ChainDone* cd;
+    ~EvFree() {
+      for (int k = 0; k < 2; k++)
+        if (cd[k].ev) hipEventDestroy(cd[k].ev);
+    }
+  } ev_free{chain_done};
   EventPair dist;
   GM_HIP(hipSetDevice(m->ctx[0]->device));
   if (int rc = dist.create()) return rc;
@@ -938,20 +1293,51 @@ int g16_prove_multi_t(gm_multi* m, gm_g16_pk_multi* mp, const uint8_t* wires, co
       }
     };
     std::lock_guard<std::recursive_mutex> g(ctx->mu);
-    if (hipSetDevice(ctx->device) != hipSuccess) return fail(GM_ERR_DEVICE);
+    if (hipSetDevice(ctx->device) != hipSuccess) {
+      if (d == chain_dev[0]) chain_done[0].signal(GM_ERR_DEVICE);
+      if (d == chain_dev[1]) chain_done[1].signal(GM_ERR_DEVICE);
+      return fail(GM_ERR_DEVICE);
+    }
     Arena arena(ctx);
-    DevBuf w, da, db, dc;
+    DevBuf w, da;
     const size_t nw = pk->whi - pk->wlo;
     int rc;
+    // a device that owns a chain must signal it even when it fails early
+    std::unique_ptr<HSource> hs;
+    if (d > 0) {
+      auto* x = new ChainRemoteH<C>(&sh, hz[d], ctx, m->ctx[0]->device, nc, pk->n);
+      const void* hv[2] = {hb, hc};
+      for (int k = 0; k < 2; k++) {
+        if (chain_dev[k] != d) continue;
+        DevBuf loc;
+        if ((rc = loc.alloc(arena, 32 * pk->n))) {
+          chain_done[k].signal(rc);
+          continue;
+        }
+        x->jobs.push_back({hv[k], loc.p, d0bc[k], &chain_done[k]});
+      }
+      hs.reset(x);
+      if (!x->jobs.empty() && (rc = x->start())) return fail(rc);
+    }
     if ((rc = w.alloc(arena, 32 * (nw ? nw : 1)))) return fail(rc);
     if (nw && hipMemcpyAsync(w.p, wires + 32 * pk->wlo, 32 * nw, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
       return fail(GM_ERR_DEVICE);
-    std::unique_ptr<HSource> hs;
-    if (d == 0) {
-      if ((rc = da.alloc(arena, 32 * pk->n)) || (rc = db.alloc(arena, 32 * pk->n)) ||
-          (rc = dc.alloc(arena, 32 * pk->n)))
-        return fail(rc);
-      auto* x = new HostStagedH<C>(ctx, pk, da.p, db.p, dc.p, ha, hb, hc, nc);
+    if (d == 0 && !split) {  // one device: computeH whole, inputs staged from the host
+      if ((rc = da.alloc(arena, 32 * pk->n))) return fail(rc);
+      auto* x = new HostStagedH<C>(ctx, pk, da.p, d0bc[0], d0bc[1], ha, hb, hc, nc);
+      hs.reset(x);
+      x->after_h = [&]() -> int {
+        GM_HIP(hipEventRecord(sh.done, ctx->aux));
+        std::lock_guard<std::mutex> lk(sh.mu);
+        sh.ready = true;
+        sh.cv.notify_all();
+        return GM_OK;
+      };
+      if ((rc = x->start())) return fail(rc);
+    } else if (d == 0) {
+      if ((rc = da.alloc(arena, 32 * pk->n))) return fail(rc);
+      auto* x = new SplitH<C>(ctx, pk, da.p, d0bc[0], d0bc[1], ha, nc);
+      x->remote = {&chain_done[0], &chain_done[1]};
       hs.reset(x);
       x->after_h = [&, x]() -> int {
         // h is produced on ctx0->aux after x->ev.b: copy the slices there too
@@ -972,8 +1358,6 @@ int g16_prove_multi_t(gm_multi* m, gm_g16_pk_multi* mp, const uint8_t* wires, co
         return GM_OK;
       };
       if ((rc = x->start())) return fail(rc);
-    } else {
-      hs.reset(new RemoteH(&sh, hz[d]));
     }
     if ((rc = g16_sums_t<C>(ctx, pk, w.p, *hs, sums[d], nullptr))) return fail(rc);
     if (d == 0) {

@@ -19,6 +19,13 @@ struct gm_g16_pk {
   bool precomp = false;         // GM_PK_PRECOMPUTE: fixed-base window copies
   gm::MsmPrecomp preA, preB, preZ, preK;  // layouts (B and B2 share preB)
   std::vector<uint8_t> alpha, beta, delta, beta2, delta2;  // host affine
+  // Shared wire plan: when the A, B (+ B2) and K arrays each cover (nearly)
+  // every wire of [wlo, whi), their MSMs read ONE digit / sort plan over the
+  // wire slice instead of one per array (g16_sums_t).  wmap[X][i] = array X's
+  // point index for wire wlo + i, or MSM_SKIP; nullptr = identity.
+  bool wshare[3] = {false, false, false};  // A, B, K
+  void* wmap[3] = {nullptr, nullptr, nullptr};
+  gm::MsmPrecomp preW;  // the wire plan's geometry (precomp: same c / W / narrow as the shared arrays)
 };
 
 namespace gm {
@@ -41,6 +48,13 @@ void pk_release(gm_g16_pk* pk);
 // gnark-layout points on the device -> internal layout at dst (+ window copies)
 int prepare_points_into(gm_ctx* ctx, int curve, bool g2, const void* gnark_dev, size_t count,
                         const MsmPrecomp* pre, void* dst);
+// Arrays (A, B, K) that qualify for the shared wire plan, from the counts alone
+// (upload and cache load decide alike): each covers >= 31/32 of the `span`
+// wires, and at least two of them do.  GM_G16_WIRE_PLAN=0 disables it.
+void wire_plan_choice(size_t span, size_t nbA, size_t nbB, size_t nbK, bool out[3]);
+// Builds pk's wire maps from the key's local compaction maps (wire - wlo per
+// point of A, B, K; host memory) and sets pk->wshare / wmap / preW.
+int pk_setup_wire_plan(gm_ctx* ctx, gm_g16_pk* pk, const uint32_t* ia, const uint32_t* ib, const uint32_t* ik);
 // src == nullptr: points from the host pointers in h
 int pk_upload_ranges(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsigned flags, const Ranges& rg,
                      gm_g16_pk** out, const PointSource* src);

@@ -624,7 +624,6 @@ int ntt_domain_prepare(gm_ctx* ctx, size_t n) {
 //   (the order pk.G1.Z uses, setup.go:265-267; icicle.go:510 reverses explicitly)
 template <class C>
 int compute_h_device(gm_ctx* ctx, void* a, void* b, void* c, size_t len, size_t n) {
-  using Fr = typename C::Fr;
   if (len > n) {
     set_error("compute_h: len > n");
     return GM_ERR_INVALID;
@@ -634,17 +633,38 @@ int compute_h_device(gm_ctx* ctx, void* a, void* b, void* c, size_t len, size_t 
     set_error("compute_h: n must be a power of two >= 2 within the 2-adicity");
     return GM_ERR_INVALID;
   }
-  hipStream_t st = ctx->stream;
-  if (len < n) {
-    for (void* v : {a, b, c}) GM_HIP(hipMemsetAsync((char*)v + 32 * len, 0, 32 * (n - len), st));
+  int rc;
+  for (void* v : {a, b, c})
+    if ((rc = compute_h_chain<C>(ctx, v, len, n))) return rc;
+  return compute_h_finish<C>(ctx, a, b, c, n);
+}
+
+// One input's chain of computeH (prove.go:372-378): pad to n, FFTInverse(DIF),
+// FFT(DIT, OnCoset) -- independent per vector, so a, b, c may run on three GPUs.
+template <class C>
+int compute_h_chain(gm_ctx* ctx, void* v, size_t len, size_t n) {
+  using Fr = typename C::Fr;
+  const int logn = log2_exact(n);
+  if (len > n || logn < 1 || logn > C::TWO_ADICITY || logn > 30) {
+    set_error("compute_h: n must be a power of two >= 2 within the 2-adicity, len <= n");
+    return GM_ERR_INVALID;
   }
+  if (len < n) GM_HIP(hipMemsetAsync((char*)v + 32 * len, 0, 32 * (n - len), ctx->stream));
   NttDomain<C>* d;
   int rc;
   if ((rc = get_domain<C>(ctx, logn, &d))) return rc;
-  for (void* v : {a, b, c}) {
-    if ((rc = transform<C>(ctx, d, v, true, false, false, NttFuse<Fr>()))) return rc;
-    if ((rc = transform<C>(ctx, d, v, false, true, true, NttFuse<Fr>()))) return rc;
-  }
+  if ((rc = transform<C>(ctx, d, v, true, false, false, NttFuse<Fr>()))) return rc;
+  return transform<C>(ctx, d, v, false, true, true, NttFuse<Fr>());
+}
+
+// The tail of computeH (prove.go:380-396) on the three chained vectors:
+// (a b - c) / (g^n - 1) fused into the coset FFTInverse(DIF) -> h in a.
+template <class C>
+int compute_h_finish(gm_ctx* ctx, void* a, const void* b, const void* c, size_t n) {
+  using Fr = typename C::Fr;
+  NttDomain<C>* d;
+  int rc;
+  if ((rc = get_domain<C>(ctx, log2_exact(n), &d))) return rc;
   NttFuse<Fr> fz;
   fz.pb = (const Fe<Fr>*)b;
   fz.pc = (const Fe<Fr>*)c;
@@ -658,6 +678,8 @@ int compute_h_device(gm_ctx* ctx, void* a, void* b, void* c, size_t len, size_t 
                                   const void*);                                           \
   template int reverse_device<C>(gm_ctx*, void*, size_t);                                 \
   template int compute_h_device<C>(gm_ctx*, void*, void*, void*, size_t, size_t);         \
+  template int compute_h_chain<C>(gm_ctx*, void*, size_t, size_t);                         \
+  template int compute_h_finish<C>(gm_ctx*, void*, const void*, const void*, size_t);      \
   template int bitrev_copy_device<C>(gm_ctx*, void*, const void*, size_t);                 \
   template int poly_ops_vec_device<C>(gm_ctx*, void*, const void*, const void*, const void*, size_t); \
   template int ntt_domain_prepare<C>(gm_ctx*, size_t);

@@ -14,6 +14,12 @@ template <class C>
 int reverse_device(gm_ctx* ctx, void* a, size_t n);
 template <class C>
 int compute_h_device(gm_ctx* ctx, void* a, void* b, void* c, size_t len, size_t n);
+// computeH in parts (a, b, c chains may run on different devices): the chain of
+// one input (pad, FFTInverse DIF, coset FFT DIT), then the fused tail -> h in a
+template <class C>
+int compute_h_chain(gm_ctx* ctx, void* v, size_t len, size_t n);
+template <class C>
+int compute_h_finish(gm_ctx* ctx, void* a, const void* b, const void* c, size_t n);
 // out[brev(i)] = in[i] (n = 2^k, out != in)
 template <class C>
 int bitrev_copy_device(gm_ctx* ctx, void* out, const void* in, size_t n);

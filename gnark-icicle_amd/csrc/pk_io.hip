@@ -448,6 +448,18 @@ int gm_g16_pk_load_cache(gm_ctx* ctx, int fd, gm_g16_pk** out) {
     }
   }
   if (hipStreamSynchronize(ctx->stream) != hipSuccess) return fail(GM_ERR_DEVICE);
+  // the shared wire plan is derived state: rebuilt from the compaction maps
+  {
+    std::vector<uint32_t> ix[3];
+    void* src[3] = {pk->idxA, pk->idxB, pk->idxK};
+    const size_t cnt[3] = {pk->nbA, pk->nbB, pk->nbK};
+    for (int x = 0; x < 3; x++) {
+      ix[x].resize(cnt[x] ? cnt[x] : 1);
+      if (cnt[x] && hipMemcpy(ix[x].data(), src[x], 4 * cnt[x], hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(GM_ERR_DEVICE);
+    }
+    if ((rc = pk_setup_wire_plan(ctx, pk, ix[0].data(), ix[1].data(), ix[2].data()))) return fail(rc);
+  }
   *out = pk;
   return GM_OK;
 }

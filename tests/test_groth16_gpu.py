@@ -233,3 +233,39 @@ def test_groth16_bsb22_commitments(gm_ctx, oracle, cname, ncommit, precompute):
     S.free()
     P.free()
     assert len(poks) == ncommit * g1b
+
+
+@pytest.mark.parametrize("precompute", [False, True])
+@pytest.mark.parametrize("shape", ["chain", "copy"])
+def test_groth16_shared_wire_plan_on_off(gm_ctx, oracle, monkeypatch, precompute, shape):
+    """The shared wire plan (one digit / sort plan over the wires for the A, B,
+    B2 and K MSMs, groth16.hip pk_setup_wire_plan) against per-array plans
+    (GM_G16_WIRE_PLAN=0): same proof, equal to the oracle's.  'chain' shares
+    A, B and K through wire maps (wires without a point are skipped entries);
+    'copy' (w_{j+1} = w_j * ONE: B holds one point) shares A and K only and B /
+    B2 keep their own plan."""
+    import gnark_mi355x as gm
+    cname = "bn254"
+    c = pyref.CURVES[cname]
+    if shape == "chain":
+        r1, W = R.squaring_chain(3000, cname, x=5)
+    else:
+        k = 3000
+        cons = [([(2 + j, 1)], [(0, 1)], [(3 + j, 1)]) for j in range(k)]
+        cons.append(([(0, 1)], [(2 + k, 1)], [(1, 1)]))
+        r1 = R.R1CS(cname, nb_public=2, nb_wires=3 + k, constraints=cons)
+        W = [1, 5] + [5] * (k + 1)
+        assert r1.is_satisfied(W)
+    tox = R.encode_vec(cname, [t % c.r for t in TOXIC])
+    pk = oracle.g16_setup(cname, r1, tox)
+    a, b, cc = r1.solve_abc(W)
+    enc = lambda v: R.encode_vec(cname, v)
+    rb, sb = enc([0xABC]), enc([0xDEF])
+    exp = oracle.g16_prove(cname, pk, r1.nb_public, enc(W), enc(a), enc(b), enc(cc), rb, sb)
+    for flag in ("1", "0"):
+        monkeypatch.setenv("GM_G16_WIRE_PLAN", flag)
+        dpk = gm.ProvingKey(gm_ctx, cname, pk, r1.domain_size, r1.nb_wires, r1.nb_public, precompute=precompute)
+        try:
+            assert dpk.prove(enc(W), enc(a), enc(b), enc(cc), rb, sb) == exp, flag
+        finally:
+            dpk.free()
