@@ -570,7 +570,8 @@ struct ChainRemoteH : RemoteH {
     return GM_OK;
   }
   int launch(bool block) {
-    if (launched || (!block && !queued.load())) return GM_OK;
+    if (launched || jobs.empty()) return GM_OK;  // devices 3.. run no chain
+    if (!block && !queued.load()) return GM_OK;
     if (th.joinable()) th.join();
     launched = true;
     int rc = copy_rc;
@@ -601,7 +602,7 @@ struct ChainRemoteH : RemoteH {
   ~ChainRemoteH() override {
     if (th.joinable()) th.join();
     if (!launched)
-      for (auto& j : jobs) j.done->signal(GM_ERR_DEVICE);  // never leave device 0 waiting
+      for (auto& j : jobs) j.done->signal(GM_ERR_DEVICE);  // never leave device 0 waiting (no-op without jobs)
     hipStreamSynchronize(ctx->copy);
     hipStreamSynchronize(ctx->aux);
     if (copied) hipEventDestroy(copied);

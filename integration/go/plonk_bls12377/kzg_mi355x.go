@@ -11,13 +11,17 @@
 //     commit(...) below: an MSM of the coefficients against the SRS kept
 //     resident on the GPU (gm_kzg_commit; same digest bytes as kzg.Commit,
 //     tests/test_msm_gpu.py::test_kzg_commit_and_prepared_msm).
-//  2. The domain1 (4n / 8n) transforms of the quotient computation
-//     (prove.go:248-262, divideByZH :539) can call gm.NTT (fft.Domain FFT /
-//     FFTInverse semantics, all DIF/DIT x coset modes; tests/test_ntt_gpu.py).
+//  2. The domain1 (4n / 8n) transform of the quotient (domains prove.go:258-263,
+//     divideByZH :1178-1205) calls gm.NTT (fft.Domain FFTInverse(DIT, OnCoset)
+//     semantics; every DIF/DIT x coset mode is tested in tests/test_ntt_gpu.py;
+//     the commit / FFT sequence is replayed in tests/test_plonk_replay_gpu.py).
 //
-// Wiring (a patch to prove.go, shown in INTEGRATION.md §5): instance gains a
-// `gpu *kzgDevice` field set in newInstance when opt.Accelerator == "icicle";
-// every `kzg.Commit(x, key...)` call becomes `s.commit(x, key)`.
+// Wiring: prove.go.diff in this directory (a real patch against the
+// reference's backend/plonk/bls12-377/prove.go; INTEGRATION.md §5): instance
+// gains `gpu *kzgDevice`, set by deviceFor(pk) in newInstance when
+// opt.Accelerator == "icicle"; every kzg.Commit goes through instance.commit;
+// divideByZH runs its domain1 FFTInverse through fftDomain1.  Without the
+// icicle tag kzg_mi355x_stub.go keeps the patched file compiling (gpu == nil).
 //
 // NOT COMPILED HERE: this image has no Go toolchain.
 package plonk
@@ -40,6 +44,20 @@ type kzgDevice struct {
 	canonical, lagr   *gm.SRS
 	canonKey, lagrKey *kzg.ProvingKey
 	err               error
+}
+
+// one kzgDevice per proving key (the SRS is uploaded once per key)
+var devices sync.Map // *ProvingKey -> *kzgDevice
+
+// deviceFor returns pk's device state, uploading its SRS on first use; nil when
+// no GPU is usable (the prover then stays on the CPU path).
+func deviceFor(pk *ProvingKey) *kzgDevice {
+	v, _ := devices.LoadOrStore(pk, &kzgDevice{})
+	d := v.(*kzgDevice)
+	if d.setup(pk) != nil {
+		return nil
+	}
+	return d
 }
 
 func (d *kzgDevice) setup(pk *ProvingKey) error {
@@ -75,8 +93,9 @@ func (d *kzgDevice) commit(p []fr.Element, key *kzg.ProvingKey) (kzg.Digest, err
 }
 
 // fftDomain1 runs the domain1 transform of prove.go's quotient on the GPU:
-// inverse selects FFTInverse, dit the DIT decimation, coset fft.OnCoset().
-func fftDomain1(v []fr.Element, inverse, dit, coset bool) error {
+// inverse selects FFTInverse, dit the DIT decimation, coset fft.OnCoset()
+// (divideByZH: FFTInverse(DIT, OnCoset), bit-reversed in, natural out).
+func (d *kzgDevice) fftDomain1(v []fr.Element, inverse, dit, coset bool) error {
 	if len(v) == 0 {
 		return nil
 	}
