@@ -177,6 +177,163 @@ Jac<F> msm_pippenger(const std::vector<std::array<uint64_t, 4>>& k, const Aff<F>
   return acc;
 }
 
+// ---------------------------------------------------------------------------
+// Signed-digit Pippenger with extended-Jacobian (XYZZ) buckets -- the shape of
+// gnark-crypto's G1Jac/G2Jac.MultiExp (signed c-bit digits, 2^(c-1) buckets
+// per window, g1JacExtended mixed adds, running-sum reduction; one task per
+// (window, chunk)).  The CPU baseline leg of bench.py times this; the unsigned
+// Jacobian version above stays as an independent cross-check.
+// ---------------------------------------------------------------------------
+template <class F>
+struct XyzzO {
+  F x, y, zz, zzz;
+};
+template <class F>
+inline XyzzO<F> xz_inf() {
+  XyzzO<F> r;
+  memset(&r, 0, sizeof(r));
+  return r;
+}
+template <class F>
+inline bool xz_is_inf(const XyzzO<F>& p) {
+  return is_zero(p.zz);
+}
+template <class F>
+inline XyzzO<F> xz_dbl_aff(const Aff<F>& q) {  // mdbl-2008-s-1, a = 0
+  F U = dbl(q.y), V = sqr(U), W = mul(U, V), S = mul(q.x, V);
+  F X2 = sqr(q.x);
+  F M = add(dbl(X2), X2);
+  F X3 = sub(sub(sqr(M), S), S);
+  F Y3 = sub(mul(M, sub(S, X3)), mul(W, q.y));
+  return {X3, Y3, V, W};
+}
+template <class F>
+inline XyzzO<F> xz_dbl(const XyzzO<F>& p) {  // dbl-2008-s-1, a = 0
+  if (xz_is_inf(p)) return p;
+  F U = dbl(p.y), V = sqr(U), W = mul(U, V), S = mul(p.x, V);
+  F X2 = sqr(p.x);
+  F M = add(dbl(X2), X2);
+  F X3 = sub(sub(sqr(M), S), S);
+  F Y3 = sub(mul(M, sub(S, X3)), mul(W, p.y));
+  return {X3, Y3, mul(V, p.zz), mul(W, p.zzz)};
+}
+template <class F>
+inline void xz_add_aff(XyzzO<F>& a, const Aff<F>& q, bool negate) {  // madd-2008-s
+  if (aff_is_inf(q)) return;
+  const Aff<F> qq = negate ? aff_neg(q) : q;
+  if (xz_is_inf(a)) {
+    a = {qq.x, qq.y, FTraits<F>::one(), FTraits<F>::one()};
+    return;
+  }
+  F P = sub(mul(qq.x, a.zz), a.x), R = sub(mul(qq.y, a.zzz), a.y);
+  if (is_zero(P)) {
+    a = is_zero(R) ? xz_dbl_aff(qq) : xz_inf<F>();
+    return;
+  }
+  F PP = sqr(P), PPP = mul(P, PP), Q = mul(a.x, PP);
+  F X3 = sub(sub(sub(sqr(R), PPP), Q), Q);
+  a.y = sub(mul(R, sub(Q, X3)), mul(a.y, PPP));
+  a.x = X3;
+  a.zz = mul(a.zz, PP);
+  a.zzz = mul(a.zzz, PPP);
+}
+template <class F>
+inline XyzzO<F> xz_add(const XyzzO<F>& a, const XyzzO<F>& b) {  // add-2008-s
+  if (xz_is_inf(a)) return b;
+  if (xz_is_inf(b)) return a;
+  F U1 = mul(a.x, b.zz), U2 = mul(b.x, a.zz), S1 = mul(a.y, b.zzz), S2 = mul(b.y, a.zzz);
+  F P = sub(U2, U1), R = sub(S2, S1);
+  if (is_zero(P)) return is_zero(R) ? xz_dbl(a) : xz_inf<F>();
+  F PP = sqr(P), PPP = mul(P, PP), Q = mul(U1, PP);
+  F X3 = sub(sub(sub(sqr(R), PPP), Q), Q);
+  F Y3 = sub(mul(R, sub(Q, X3)), mul(S1, PPP));
+  return {X3, Y3, mul(mul(a.zz, b.zz), PP), mul(mul(a.zzz, b.zzz), PPP)};
+}
+// (X, Y, ZZ, ZZZ) -> Jacobian with Z = ZZ ZZZ: X' = X ZZ ZZZ^2, Y' = Y ZZ^3 ZZZ^2
+template <class F>
+inline Jac<F> xz_to_jac(const XyzzO<F>& p) {
+  if (xz_is_inf(p)) return jac_inf<F>();
+  F z3sq = sqr(p.zzz), zz3 = mul(sqr(p.zz), p.zz);
+  return {mul(mul(p.x, p.zz), z3sq), mul(mul(p.y, zz3), z3sq), mul(p.zz, p.zzz)};
+}
+
+template <class C, class F>
+Jac<F> msm_pippenger_signed(const std::vector<std::array<uint64_t, 4>>& k, const Aff<F>* pts, size_t n,
+                            int nthreads) {
+  if (n == 0) return jac_inf<F>();
+  int lg = 0;
+  while ((1ull << (lg + 1)) <= n) lg++;
+  // window: n W adds + 2^c reduction adds per window and chunk (gnark-crypto's
+  // bestC minimises the same kind of cost)
+  int c = 2;
+  double best = 1e300;
+  for (int cc = 2; cc <= 16; cc++) {
+    const double W = (C::nbits + 1 + cc - 1) / cc;
+    const double cost = W * ((double)n + 2.0 * (double)(1u << (cc - 1)));
+    if (cost < best) {
+      best = cost;
+      c = cc;
+    }
+  }
+  const int W = (C::nbits + 1 + c - 1) / c;  // signed digits: the top one never carries
+  const uint32_t half = 1u << (c - 1);
+  // signed digits, window-major: d in [-2^(c-1), 2^(c-1)]
+  std::vector<int32_t> dig((size_t)W * n);
+  parallel_for(n, nthreads, [&](size_t s, size_t e) {
+    for (size_t i = s; i < e; i++) {
+      uint32_t carry = 0;
+      for (int w = 0; w < W; w++) {
+        const int bit = w * c;
+        uint32_t raw = bit < 256 ? get_window(k[i].data(), bit, std::min(c, 256 - bit)) : 0;
+        raw += carry;
+        if (raw > half) {
+          dig[(size_t)w * n + i] = (int32_t)raw - (int32_t)(1u << c);
+          carry = 1;
+        } else {
+          dig[(size_t)w * n + i] = (int32_t)raw;
+          carry = 0;
+        }
+      }
+    }
+  });
+  int nchunks = std::max(1, (2 * nthreads + W - 1) / W);
+  if ((size_t)nchunks > n) nchunks = (int)n;
+  const size_t chunk = (n + nchunks - 1) / nchunks;
+  std::vector<XyzzO<F>> partial((size_t)W * nchunks, xz_inf<F>());
+  std::atomic<int> next(0);
+  auto worker = [&]() {
+    std::vector<XyzzO<F>> buckets(half);
+    for (;;) {
+      const int task = next.fetch_add(1);
+      if (task >= W * nchunks) break;
+      const int w = task / nchunks, ch = task % nchunks;
+      const size_t s = ch * chunk, e = std::min(n, s + chunk);
+      std::fill(buckets.begin(), buckets.end(), xz_inf<F>());
+      const int32_t* dw = dig.data() + (size_t)w * n;
+      for (size_t i = s; i < e; i++) {
+        const int32_t d = dw[i];
+        if (d > 0) xz_add_aff(buckets[d - 1], pts[i], false);
+        else if (d < 0) xz_add_aff(buckets[-d - 1], pts[i], true);
+      }
+      XyzzO<F> run = xz_inf<F>(), tot = xz_inf<F>();
+      for (size_t b = half; b-- > 0;) {
+        run = xz_add(run, buckets[b]);
+        tot = xz_add(tot, run);
+      }
+      partial[(size_t)w * nchunks + ch] = tot;
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 0; t < std::max(1, nthreads); t++) th.emplace_back(worker);
+  for (auto& x : th) x.join();
+  XyzzO<F> acc = xz_inf<F>();
+  for (int w = W - 1; w >= 0; w--) {
+    for (int i = 0; i < c; i++) acc = xz_dbl(acc);
+    for (int ch = 0; ch < nchunks; ch++) acc = xz_add(acc, partial[(size_t)w * nchunks + ch]);
+  }
+  return xz_to_jac(acc);
+}
+
 template <class C>
 std::vector<std::array<uint64_t, 4>> canon_scalars(const uint8_t* scalars, size_t n, int nthreads) {
   using Fr = typename C::Fr;
@@ -196,11 +353,13 @@ int msm_impl(const uint8_t* scalars, const uint8_t* points, size_t n, int nthrea
   auto k = canon_scalars<C>(scalars, n, nthreads);
   const Aff<F>* pts = reinterpret_cast<const Aff<F>*>(points);
   Jac<F> r;
-  if (naive) {
+  if (naive == 1) {
     r = jac_inf<F>();
     for (size_t i = 0; i < n; i++) r = jadd(r, scalar_mul(to_jac(pts[i]), k[i].data(), 4));
-  } else {
+  } else if (naive == 2) {  // unsigned-digit Jacobian Pippenger (cross-check)
     r = msm_pippenger<C, F>(k, pts, n, nthreads);
+  } else {
+    r = msm_pippenger_signed<C, F>(k, pts, n, nthreads);
   }
   store_aff(out, to_aff(r));
   return 0;

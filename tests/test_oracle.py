@@ -215,3 +215,20 @@ def test_oracle_groth16_bsb22_verifies(oracle, cname, ncommit):
     ar, bs, krs = oracle.g16_prove(cname, full, r1.nb_public, pr["Wb"], pr["a"], pr["b"], pr["c"], pr["rb"], pr["sb"])
     nf = dict(pr, ar=ar, bs=bs, krs=krs)
     assert not oracle.bsb22_check(cname, r1, pk, info, nf, sig)
+
+
+@pytest.mark.parametrize("cname,g2", [("bn254", False), ("bn254", True), ("bls12377", False), ("bls12377", True)])
+def test_oracle_signed_pippenger_vs_unsigned(oracle, cname, g2):
+    """The default oracle MSM (signed digits, XYZZ buckets: gnark-crypto
+    MultiExp's shape; the bench's CPU baseline) against the unsigned-digit
+    Jacobian Pippenger (naive=2), edge scalars included."""
+    c = pyref.CURVES[cname]
+    for n in (1, 7, 300, 2049):
+        sc = pyref.random_scalars(c, n, n + 11)
+        sc[0] = c.r - 1
+        if n > 3:
+            sc[1], sc[2] = 0, 1
+        sb = R.encode_vec(cname, sc)
+        pts = oracle.batch_mul_base(cname, g2, oracle.generator(cname, g2),
+                                    R.encode_vec(cname, pyref.random_scalars(c, n, n + 12)))
+        assert oracle.msm(cname, g2, sb, pts) == oracle.msm(cname, g2, sb, pts, naive=2), n
