@@ -270,6 +270,8 @@ def secondary(ctx, gm, args):
     res["ntt"] = {"logn": args.ntt_logn, "gelem_per_s": round(nn / dt / 1e9, 4), "ms_per_transform": round(dt * 1e3, 4),
                   "achieved_gbs": round(gbs, 1), "frac_hbm": round(gbs / HBM_PEAK_GBS, 4),
                   "avg_pass_ms": round(avg_pass, 4), "passes_per_transform": round(pass_cnt / (2 * reps), 2)}
+    if not args.no_cpu_baseline:
+        res["ntt"]["cpu_baseline"] = ntt_cpu_baseline(ctx, min(args.ntt_logn, 22))
     if args.msm_extra:
         res["msm"] = {}
         for curve, g2, logn in (("bn254", True, 20), ("bls12377", False, 22), ("bls12377", True, 22)):
@@ -391,11 +393,22 @@ def groth16_bench(ctx, gm, logn, precompute=True, check_oracle=False):
     if check_oracle:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle_lib
+        threads, model = host_cpu()
         pk["sizes"] = np.array([n, nb_wires, nb_wires, nb_wires, nb_wires - nb_public], np.uint64)
         t0 = time.perf_counter()
-        exp = oracle_lib.g16_prove("bn254", pk, nb_public, host[0], host[1], host[2], host[3], r[:32], r[32:])
-        res["oracle_s"] = round(time.perf_counter() - t0, 2)
+        exp = oracle_lib.g16_prove("bn254", pk, nb_public, host[0], host[1], host[2], host[3], r[:32], r[32:],
+                                   nthreads=threads)
+        cpu_s = time.perf_counter() - t0
         res["matches_oracle"] = bool(exp == proof)
+        # the labelled CPU baseline of this workload (BASELINE.md §2.1 asks for
+        # groth16_bn254.Prove beside the GPU; no Go on the box -> the port)
+        res["cpu_baseline"] = {
+            "value": round(cpu_s * 1e3, 1), "unit": "ms per proof", "cores": threads, "kind": "port",
+            "cpu_model": model,
+            "sample": "one full 2^%d Groth16 prove on the same key and inputs (computeH + 4 G1 + 1 G2 "
+                      "signed-digit Pippenger MSMs + finishing adds): oracle/gm_oracle.cpp restatement of "
+                      "prove.go:62-325, not gnark-crypto (no Go toolchain on the box)" % logn,
+            "gpu_over_cpu": round(cpu_s * 1e3 / max(res["prove_ms_host_inputs"], 1e-9), 1)}
     return res
 
 
@@ -585,6 +598,26 @@ def groth16_multi_bench(ctx, gm, logn, ndev, precompute=True):
             "note": "one process, one host thread per GPU (gm_multi); computeH on GPU 0, h slices peer-copied"}
 
 
+def ntt_cpu_baseline(ctx, logn):
+    """Oracle radix-2 FFT (fft.Domain.FFT restatement, oracle/gm_oracle.cpp) on the
+    box's CPU share: forward DIF + inverse DIT of a 2^logn vector (bounded
+    sample; the GPU line is 2^24)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_lib
+    threads, model = host_cpu()
+    n = 1 << logn
+    X = ctx.random_scalars("bn254", n, 7)
+    xb = X.to_host()
+    X.free()
+    t0 = time.perf_counter()
+    y = oracle_lib.fft("bn254", xb, False, False, False, nthreads=threads)
+    z = oracle_lib.fft("bn254", y, True, True, False, nthreads=threads)
+    dt = (time.perf_counter() - t0) / 2
+    return {"value": round(n / dt / 1e9, 4), "unit": "Gelem/s", "cores": threads, "kind": "port", "cpu_model": model,
+            "sample": "2^%d BN254 Fr FFT + FFTInverse round trip (oracle restatement of fft.Domain, not "
+                      "gnark-crypto)" % logn, "round_trip_ok": bool(z == xb)}
+
+
 def cpu_baseline(S, P, n, gpu_jac):
     """Oracle C++ Pippenger (the 'port') on the host cores this process may use
     (the box's CPU share), same 2^logn workload incl. the edge set, checked
@@ -606,8 +639,9 @@ def cpu_baseline(S, P, n, gpu_jac):
     match = gm.jac_to_affine("bn254", False, gpu_jac) == aff
     return {"value": round(n / dt / 1e6, 4), "unit": "Mpoints/s", "cores": threads, "kind": "port",
             "cpu_model": model,
-            "sample": "full 2^%d-point BN254 G1 MSM (same input, edge set incl.), %d rep(s), C++ Pippenger "
-                      "restatement (oracle/), not gnark-crypto (no Go toolchain on the box)"
+            "sample": "full 2^%d-point BN254 G1 MSM (same input, edge set incl.), %d rep(s), C++ signed-digit "
+                      "XYZZ-bucket Pippenger (gnark-crypto MultiExp's shape, oracle/), not gnark-crypto (no Go "
+                      "toolchain on the box)"
                       % (n.bit_length() - 1, reps),
             "result_matches_gpu": bool(match)}
 

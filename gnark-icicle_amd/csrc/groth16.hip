@@ -338,13 +338,20 @@ struct HSource {
 // computeH on the context's auxiliary stream, overlapped with the MSMs (whose
 // sorts, reductions and host round trips leave the VALUs idle).
 // GM_G16_OVERLAP=0 runs it in order on the main stream (A/B measurements).
+// r1: a, b, c are first evaluated from the wires by the device-resident R1CS
+// (gm_g16_prove_r1cs), on the same stream as computeH.
 template <class C>
 int launch_compute_h(gm_ctx* ctx, void* a, void* b, void* c, size_t nc, size_t n, hipEvent_t wait_for,
-                     hipEvent_t done) {
+                     hipEvent_t done, const gm_r1cs* r1 = nullptr, const void* wires = nullptr) {
   static const bool overlap = !getenv("GM_G16_OVERLAP") || atoi(getenv("GM_G16_OVERLAP")) != 0;
+  auto body = [&]() -> int {
+    int rc;
+    if (r1 && (rc = r1cs_eval_device(ctx, r1, wires, a, b, c))) return rc;
+    return compute_h_device<C>(ctx, a, b, c, nc, n);
+  };
   if (!overlap) {
     if (wait_for) GM_HIP(hipStreamWaitEvent(ctx->stream, wait_for, 0));
-    int rc = compute_h_device<C>(ctx, a, b, c, nc, n);
+    int rc = body();
     if (rc) return rc;
     GM_HIP(hipEventRecord(done, ctx->stream));
     return GM_OK;
@@ -352,7 +359,7 @@ int launch_compute_h(gm_ctx* ctx, void* a, void* b, void* c, size_t nc, size_t n
   if (wait_for) GM_HIP(hipStreamWaitEvent(ctx->aux, wait_for, 0));
   hipStream_t main = ctx->stream;
   ctx->stream = ctx->aux;
-  int rc = compute_h_device<C>(ctx, a, b, c, nc, n);
+  int rc = body();
   ctx->stream = main;
   if (rc) return rc;
   GM_HIP(hipEventRecord(done, ctx->aux));
@@ -379,13 +386,15 @@ struct DeviceH : HSource {
   gm_g16_pk* pk;
   void *a, *b, *c;
   size_t nc;
+  const gm_r1cs* r1 = nullptr;  // set: a, b, c evaluated from `wires` first
+  const void* wires = nullptr;
   EventPair ev;  // a: inputs ready (main stream), b: h ready
   DeviceH(gm_ctx* x, gm_g16_pk* k, void* a_, void* b_, void* c_, size_t n_) : ctx(x), pk(k), a(a_), b(b_), c(c_), nc(n_) {}
   int start() {
     int rc;
     if ((rc = ev.create())) return rc;
     GM_HIP(hipEventRecord(ev.a, ctx->stream));
-    return launch_compute_h<C>(ctx, a, b, c, nc, pk->n, ev.a, ev.b);
+    return launch_compute_h<C>(ctx, a, b, c, nc, pk->n, ev.a, ev.b, r1, wires);
   }
   int z_scalars(const void** zs) override {
     GM_HIP(hipStreamWaitEvent(ctx->stream, ev.b, 0));
@@ -874,7 +883,7 @@ G16Finish<C>* make_finish(const gm_g16_pk* pk, const void* r, const void* s) {
 template <class C>
 int g16_prove_t(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, void* a, void* b, void* c, const void* ha,
                 const void* hb, const void* hc, size_t nc, const void* r, const void* s, void* ar_out, void* bs_out,
-                void* krs_out) {
+                void* krs_out, const gm_r1cs* r1 = nullptr) {
   std::unique_ptr<G16Finish<C>> fin(make_finish<C>(pk, r, s));
   fin->begin();
   std::unique_ptr<HSource> hs;
@@ -885,6 +894,8 @@ int g16_prove_t(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, void* a, void
     rc = x->start();
   } else {
     auto* x = new DeviceH<C>(ctx, pk, a, b, c, nc);
+    x->r1 = r1;
+    x->wires = wires_dev;
     hs.reset(x);
     rc = x->start();
   }
@@ -1024,6 +1035,35 @@ int gm_g16_prove(gm_ctx* ctx, gm_g16_pk* pk, const void* wires, const void* a, c
                                                        bs_out, krs_out)
                              : g16_prove_t<CurveBLS12377>(ctx, pk, w.p, da.p, db.p, dc.p, a, b, c, nc, r, s, ar_out,
                                                           bs_out, krs_out);
+  prof_collect(ctx);
+  return rc;
+}
+
+// Wires alone in host memory, the R1CS resident (gm_r1cs_upload): the wires
+// are copied, a / b / c evaluated on the device (auxiliary stream, ahead of
+// computeH) while the A/B/K MSMs run on the main stream.
+int gm_g16_prove_r1cs(gm_ctx* ctx, gm_g16_pk* pk, const gm_r1cs* r1, const void* wires, const void* r,
+                      const void* s, void* ar_out, void* bs_out, void* krs_out) {
+  if (!ctx || !pk || !r1 || !wires || !r || !s || !ar_out || !bs_out || !krs_out) return GM_ERR_INVALID;
+  const size_t nc = r1cs_nb_constraints(r1);
+  if (nc > pk->n || r1cs_nb_wires(r1) != pk->nb_wires || pk->wlo != 0 || pk->whi != pk->nb_wires) {
+    set_error("prove_r1cs: constraint system does not match the proving key (constraints <= n, same wires, "
+              "whole key)");
+    return GM_ERR_INVALID;
+  }
+  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  GM_HIP(hipSetDevice(ctx->device));
+  Arena arena(ctx);
+  DevBuf w, da, db, dc;
+  int rc;
+  if ((rc = w.alloc(arena, 32 * pk->nb_wires)) || (rc = da.alloc(arena, 32 * pk->n)) ||
+      (rc = db.alloc(arena, 32 * pk->n)) || (rc = dc.alloc(arena, 32 * pk->n)))
+    return rc;
+  GM_HIP(hipMemcpyAsync(w.p, wires, 32 * pk->nb_wires, hipMemcpyHostToDevice, ctx->stream));
+  rc = pk->curve == GM_BN254 ? g16_prove_t<CurveBN254>(ctx, pk, w.p, da.p, db.p, dc.p, nullptr, nullptr, nullptr, nc,
+                                                       r, s, ar_out, bs_out, krs_out, r1)
+                             : g16_prove_t<CurveBLS12377>(ctx, pk, w.p, da.p, db.p, dc.p, nullptr, nullptr, nullptr,
+                                                          nc, r, s, ar_out, bs_out, krs_out, r1);
   prof_collect(ctx);
   return rc;
 }

@@ -55,6 +55,11 @@ void wire_plan_choice(size_t span, size_t nbA, size_t nbB, size_t nbK, bool out[
 // Builds pk's wire maps from the key's local compaction maps (wire - wlo per
 // point of A, B, K; host memory) and sets pk->wshare / wmap / preW.
 int pk_setup_wire_plan(gm_ctx* ctx, gm_g16_pk* pk, const uint32_t* ia, const uint32_t* ib, const uint32_t* ik);
+// a, b, c = <L_i, w>, <R_i, w>, <O_i, w> of a device-resident R1CS (r1cs.hip),
+// queued on ctx->stream
+int r1cs_eval_device(gm_ctx* ctx, const gm_r1cs* r, const void* wires_dev, void* a, void* b, void* c);
+size_t r1cs_nb_constraints(const gm_r1cs* r);
+size_t r1cs_nb_wires(const gm_r1cs* r);
 // src == nullptr: points from the host pointers in h
 int pk_upload_ranges(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsigned flags, const Ranges& rg,
                      gm_g16_pk** out, const PointSource* src);

@@ -53,7 +53,8 @@ SYMBOLS = [
     "gm_multi_context", "gm_g16_pk_upload_multi", "gm_g16_pk_free_multi", "gm_g16_prove_multi",
     "gm_g16_pk_upload_dump", "gm_g16_pk_upload_dump_shard", "gm_g16_pk_save_cache", "gm_g16_pk_load_cache",
     "gm_g16_stage_begin", "gm_g16_stage_put_range", "gm_g16_stage_put_indexed", "gm_g16_stage_prove",
-    "gm_g16_stage_free", "gm_msm_async", "gm_msm_wait",
+    "gm_g16_stage_free", "gm_msm_async", "gm_msm_wait", "gm_r1cs_upload", "gm_r1cs_free", "gm_r1cs_eval",
+    "gm_g16_prove_r1cs",
 ]
 
 
@@ -112,6 +113,10 @@ def load_library(path: str = LIB_PATH):
     L.gm_g16_pk_free.argtypes = [vp, vp]
     L.gm_g16_prove.argtypes = [vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, vp, vp]
     L.gm_g16_prove_device.argtypes = [vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, vp, vp]
+    L.gm_r1cs_upload.argtypes = [vp, i, sz, sz, vp, vp, vp, vp, sz, vp]
+    L.gm_r1cs_free.argtypes = [vp, vp]
+    L.gm_r1cs_eval.argtypes = [vp, vp, vp, vp, vp, vp]
+    L.gm_g16_prove_r1cs.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.gm_jac_add.argtypes = [i, i, vp, vp, vp]
     L.gm_jac_to_affine.argtypes = [i, i, vp, vp]
     L.gm_batch_mul_base.argtypes = [vp, i, i, vp, vp, sz, vp]
@@ -679,6 +684,17 @@ class ProvingKey:
                                            A.size // FR_BYTES, _p(R), _p(S), _p(ar), _p(bs), _p(krs)))
         return ar.tobytes(), bs.tobytes(), krs.tobytes()
 
+    def prove_r1cs(self, r1cs: "R1CS", wires, r: bytes, s: bytes):
+        """gm_g16_prove_r1cs: the wires are the only host input; a, b, c come
+        from the device-resident constraint system."""
+        W, R, S = (_buf(x) for x in (wires, r, s))
+        ar = np.zeros(point_bytes(self.curve, False), np.uint8)
+        krs = np.zeros(point_bytes(self.curve, False), np.uint8)
+        bs = np.zeros(point_bytes(self.curve, True), np.uint8)
+        _check(load_library().gm_g16_prove_r1cs(self.ctx.handle, self.handle, r1cs.handle, _p(W), _p(R), _p(S),
+                                                _p(ar), _p(bs), _p(krs)))
+        return ar.tobytes(), bs.tobytes(), krs.tobytes()
+
     def prove_device(self, wires: DeviceBuffer, a: DeviceBuffer, b: DeviceBuffer, c: DeviceBuffer,
                      nb_constraints: int, r: bytes, s: bytes):
         R, S = _buf(r), _buf(s)
@@ -782,6 +798,61 @@ class Multi:
 
     def __exit__(self, *a):
         self.close()
+
+
+R1CS_CONST = 0xFFFFFFFF  # GM_R1CS_CONST: a constant term (constraint.Term.IsConstant)
+
+
+class R1CS:
+    """A constraint system resident on the device (gm_r1cs_upload): per matrix
+    L, R, O a CSR of (coefficient id, wire id) terms over a coefficient table
+    (gnark's CoeffTable: id 0 = 0, 1 = 1, 2 = 2, 3 = -1, 4 = -2, then the
+    circuit's own).  from_terms builds the table from per-term coefficients."""
+
+    def __init__(self, ctx: Context, curve, nb_constraints: int, nb_wires: int, rowptr, cid, vid, coeffs: bytes):
+        self.ctx = ctx
+        self.curve = curve_id(curve)
+        self.nc, self.nb_wires = nb_constraints, nb_wires
+        rp = [np.ascontiguousarray(np.asarray(x, np.uint32)) for x in rowptr]
+        ci = [np.ascontiguousarray(np.asarray(x if len(x) else [0], np.uint32)) for x in cid]
+        vi = [np.ascontiguousarray(np.asarray(x if len(x) else [0], np.uint32)) for x in vid]
+        co = _buf(coeffs)
+        arr = lambda xs: (ctypes.c_void_p * 3)(*[x.ctypes.data for x in xs])
+        handle = ctypes.c_void_p()
+        _check(load_library().gm_r1cs_upload(ctx.handle, self.curve, nb_constraints, nb_wires, arr(rp), arr(ci),
+                                             arr(vi), _p(co), co.size // FR_BYTES, ctypes.byref(handle)))
+        self.handle = handle
+
+    @classmethod
+    def from_terms(cls, ctx: Context, curve, nb_constraints: int, nb_wires: int, rowptr, wires, coeffs, modulus: int):
+        """rowptr / wires / coeffs per matrix as in tests/r1cs.R1CS (coeffs: 32-byte
+        Montgomery values per term)."""
+        R = (1 << 256) % modulus
+        enc = lambda v: (v * R % modulus).to_bytes(32, "little")
+        table = [enc(0), enc(1), enc(2), enc(modulus - 1), enc(modulus - 2)]
+        index = {t: k for k, t in enumerate(table)}
+        cid = []
+        for m in range(3):
+            cb = bytes(np.asarray(coeffs[m], np.uint8).tobytes())
+            nt = int(rowptr[m][-1])
+            ids = []
+            for q in range(nt):
+                t = cb[32 * q:32 * q + 32]
+                if t not in index:
+                    index[t] = len(table)
+                    table.append(t)
+                ids.append(index[t])
+            cid.append(ids)
+        vid = [list(np.asarray(wires[m], np.uint32)[:int(rowptr[m][-1])]) for m in range(3)]
+        return cls(ctx, curve, nb_constraints, nb_wires, rowptr, cid, vid, b"".join(table))
+
+    def eval(self, wires: DeviceBuffer, a: DeviceBuffer, b: DeviceBuffer, c: DeviceBuffer):
+        _check(load_library().gm_r1cs_eval(self.ctx.handle, self.handle, wires.ptr, a.ptr, b.ptr, c.ptr))
+
+    def free(self):
+        if self.handle:
+            load_library().gm_r1cs_free(self.ctx.handle, self.handle)
+            self.handle = None
 
 
 class ProvingKeyMulti:

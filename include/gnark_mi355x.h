@@ -241,6 +241,30 @@ int gm_g16_prove_device(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, void*
                         void* b_dev, void* c_dev, size_t nb_constraints, const void* r,
                         const void* s, void* ar_out, void* bs_out, void* krs_out);
 
+/* ---- R1CS resident on the device: a proof from the wires alone ------------
+ * gnark's solver produces solution.A/B/C as <L_i, w>, <R_i, w>, <O_i, w>
+ * (constraint/bn254/solver.go:540-620); with the constraint system on the
+ * device (uploaded once, like the key) only the wires cross PCIe per proof.
+ * Per matrix m in {L, R, O}: rowptr[m] (nb_constraints + 1 entries, from 0),
+ * cid[m] / vid[m] (rowptr[m][nb_constraints] terms: coefficient id into
+ * `coeffs`, wire id, or GM_R1CS_CONST for a constant term -- constraint.Term,
+ * constraint/term.go:31-40); coeffs = the CoeffTable (coeff.go:30-44,
+ * ncoeffs fr.Element, Montgomery; ids 0 and 1 must be zero and one).  Ids are
+ * validated at upload. */
+#define GM_R1CS_CONST 0xFFFFFFFFu
+typedef struct gm_r1cs gm_r1cs;
+int gm_r1cs_upload(gm_ctx* ctx, int curve, size_t nb_constraints, size_t nb_wires, const uint32_t* const* rowptr,
+                   const uint32_t* const* cid, const uint32_t* const* vid, const void* coeffs, size_t ncoeffs,
+                   gm_r1cs** out);
+int gm_r1cs_free(gm_ctx* ctx, gm_r1cs* r1cs);
+/* a_dev, b_dev, c_dev (nb_constraints Fr each) from device-resident wires. */
+int gm_r1cs_eval(gm_ctx* ctx, const gm_r1cs* r1cs, const void* wires_dev, void* a_dev, void* b_dev, void* c_dev);
+/* gm_g16_prove with the wires as the only host input: wires copied, a / b / c
+ * evaluated on the device ahead of computeH while the MSMs run.  The key must
+ * be whole (not a shard) and match the constraint system. */
+int gm_g16_prove_r1cs(gm_ctx* ctx, gm_g16_pk* pk, const gm_r1cs* r1cs, const void* wires, const void* r,
+                      const void* s, void* ar_out, void* bs_out, void* krs_out);
+
 /* ---- sharded Groth16 (BASELINE config 4: G1/G2 MSMs split across the GPUs of
  *      a node, one process per GPU) -------------------------
  * Rank `rank` of `world` uploads only its contiguous slice [lo, hi) of each
