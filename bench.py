@@ -315,6 +315,22 @@ def msm_line(ctx, gm, curve, g2, logn, reps=5, precompute=False):
     return {"mpoints_per_s": round(n / dt / 1e6, 3), "ms": round(dt * 1e3, 3)}
 
 
+def chain_r1cs(ctx, gm, n, nb_wires):
+    """Device-resident squaring-chain R1CS with n constraints over nb_wires = n + 2
+    wires (one term per matrix and row, coefficient id 1 = one)."""
+    import numpy as np
+    assert nb_wires == n + 2
+    j = np.arange(n - 1, dtype=np.uint32)
+    rp = np.arange(n + 1, dtype=np.uint32)
+    vl = np.concatenate([2 + j, np.array([0], np.uint32)])
+    vr = np.concatenate([2 + j, np.array([n + 1], np.uint32)])
+    vo = np.concatenate([3 + j, np.array([1], np.uint32)])
+    ones = np.ones(n, np.uint32)
+    enc = lambda v: (v * (1 << 256) % R_BN254).to_bytes(32, "little")
+    table = b"".join(enc(v) for v in (0, 1, 2, R_BN254 - 1, R_BN254 - 2))
+    return gm.R1CS(ctx, "bn254", n, nb_wires, [rp, rp, rp], [ones, ones, ones], [vl, vr, vo], table)
+
+
 def synthetic_pk(ctx, gm, n, nb_wires, nb_public, slices=None):
     """Synthetic proving key of random points (the DummySetup-style timing key of
     groth16_test.go:70-88; a real setup at 2^24 is out of reach here).  slices:
@@ -379,12 +395,25 @@ def groth16_bench(ctx, gm, logn, precompute=True, check_oracle=False):
         t0 = time.perf_counter()
         proof = dpk.prove(host[0], host[1], host[2], host[3], r[:32], r[32:])
         t_host.append(time.perf_counter() - t0)
+    # R1CS resident (gm_r1cs_upload, once): the squaring chain of
+    # groth16_test.go:120-156 over these nb_wires wires (row i: w_{2+i} * w_{2+i}
+    # = w_{3+i}, last row 1 * w_{n+1} = Y); per proof only the wires cross PCIe
+    ch = chain_r1cs(ctx, gm, n, nb_wires)
+    t_r1cs, proof_r1cs = [], None
+    for _ in range(reps):
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        proof_r1cs = dpk.prove_r1cs(ch, host[0], r[:32], r[32:])
+        t_r1cs.append(time.perf_counter() - t0)
+    ch.free()
     med = lambda v: sorted(v)[len(v) // 2]
     res = {"logn": logn, "pk": "precomputed" if precompute else "plain",
            "prove_ms_host_inputs": round(med(t_host) * 1e3, 3), "prove_ms_device_inputs": round(med(t_dev) * 1e3, 3),
+           "prove_ms_r1cs_resident": round(med(t_r1cs) * 1e3, 3),
            "runs": reps, "stat": "median",
            "scope": "host_inputs = icicle.go:204-412 incl. H2D of wires/a/b/c; device_inputs = same with inputs "
-                    "resident; both after Solve"}
+                    "resident; r1cs_resident = host wires only (a/b/c from the device-resident R1CS, "
+                    "gm_g16_prove_r1cs); all after Solve"}
     if check_oracle:
         res.update(staged_and_io_bench(ctx, gm, dpk, pk, n, nb_wires, nb_public, host, r, proof))
     dpk.free()
@@ -400,6 +429,14 @@ def groth16_bench(ctx, gm, logn, precompute=True, check_oracle=False):
                                    nthreads=threads)
         cpu_s = time.perf_counter() - t0
         res["matches_oracle"] = bool(exp == proof)
+        # the R1CS-resident proof: a, b, c of the chain from the same wires
+        wv = host[0].reshape(nb_wires, 32)
+        ca = np.concatenate([wv[2:n + 1], wv[0:1]])
+        cb = np.concatenate([wv[2:n + 1], wv[n + 1:n + 2]])
+        cc = np.concatenate([wv[3:n + 2], wv[1:2]])
+        exp_r1cs = oracle_lib.g16_prove("bn254", pk, nb_public, host[0], ca.tobytes(), cb.tobytes(), cc.tobytes(),
+                                        r[:32], r[32:], nthreads=threads)
+        res["r1cs_resident_matches_oracle"] = bool(exp_r1cs == proof_r1cs)
         # the labelled CPU baseline of this workload (BASELINE.md §2.1 asks for
         # groth16_bn254.Prove beside the GPU; no Go on the box -> the port)
         res["cpu_baseline"] = {

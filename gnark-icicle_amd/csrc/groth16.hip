@@ -42,21 +42,6 @@ int check_curve_id(int curve) {
 }
 
 namespace {
-// Entries of the shared wire plan -> entries of array X: value w * sin + i
-// (wire i of window copy w; sin = 0 for plain layouts) becomes
-// w * sout + map[i], or MSM_SKIP when X has no point for wire i.
-__global__ void k_map_plan_vals(const uint32_t* __restrict__ vals, const uint32_t* __restrict__ offsets,
-                                uint32_t total, size_t M, const uint32_t* __restrict__ map, uint32_t sin,
-                                uint32_t sout, uint32_t* __restrict__ out) {
-  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= M || j >= offsets[total]) return;
-  const uint32_t v = vals[j];
-  const uint32_t raw = v & 0x7fffffffu;
-  const uint32_t w = sin ? raw / sin : 0u;
-  const uint32_t m = map[raw - w * sin];
-  out[j] = (m == MSM_SKIP ? MSM_SKIP : w * sout + m) | (v & 0x80000000u);
-}
-
 // dst[i] = src[idx[i]] (Fr, 32 bytes) -- device-side scalar compaction
 __global__ void k_gather_fr(const uint4* __restrict__ src, const uint32_t* __restrict__ idx, size_t n,
                             uint4* __restrict__ dst) {
@@ -94,8 +79,7 @@ size_t internal_point_bytes(int curve, bool g2) {
 }
 
 void pk_release(gm_g16_pk* pk) {
-  for (void* q : {pk->A, pk->B, pk->Z, pk->K, pk->B2, pk->idxA, pk->idxB, pk->idxK, pk->wmap[0], pk->wmap[1],
-                  pk->wmap[2]})
+  for (void* q : {pk->A, pk->B, pk->Z, pk->K, pk->B2, pk->idxA, pk->idxB, pk->idxK})
     if (q) hipFree(q);
   delete pk;
 }
@@ -113,59 +97,37 @@ void wire_plan_choice(size_t span, size_t nbA, size_t nbB, size_t nbK, bool out[
     for (int x = 0; x < 3; x++) out[x] = false;
 }
 
-int pk_setup_wire_plan(gm_ctx* ctx, gm_g16_pk* pk, const uint32_t* ia, const uint32_t* ib, const uint32_t* ik) {
-  const size_t span = pk->whi - pk->wlo;
-  bool want[3];
-  wire_plan_choice(span, pk->nbA, pk->nbB, pk->nbK, want);
-  const int frbits = pk->curve == GM_BN254 ? CurveBN254::FR_BITS : CurveBLS12377::FR_BITS;
-  MsmPrecomp pw;
-  if (pk->precomp) {
-    pw = msm_choose_precomp(span, frbits);
-    pw.stride = span;
-  }
-  const uint32_t* idx[3] = {ia, ib, ik};
-  const size_t cnt[3] = {pk->nbA, pk->nbB, pk->nbK};
-  const MsmPrecomp* pre[3] = {&pk->preA, &pk->preB, &pk->preK};
-  std::vector<uint32_t> map[3];
-  bool ident[3] = {false, false, false};
+void wire_plan_maps(size_t span, const uint32_t* const idx[3], const size_t cnt[3], bool want[3],
+                    std::vector<uint32_t> map[3]) {
   int k = 0;
   for (int x = 0; x < 3; x++) {
     if (!want[x]) continue;
-    // a precomputed array must have the plan's window geometry
-    if (pk->precomp && (pre[x]->c != pw.c || pre[x]->W != pw.W || pre[x]->narrow != pw.narrow)) {
-      want[x] = false;
-      continue;
-    }
     map[x].assign(span, MSM_SKIP);
-    bool ok = true;
-    for (size_t j = 0; j < cnt[x] && ok; j++) {
+    for (size_t j = 0; j < cnt[x] && want[x]; j++) {
       const uint32_t w = idx[x][j];
-      if (w >= span || map[x][w] != MSM_SKIP) ok = false;  // a wire used twice: own plan
+      if (w >= span || map[x][w] != MSM_SKIP) want[x] = false;  // a wire used twice: own plan
       else map[x][w] = (uint32_t)j;
     }
-    if (!ok) {
-      want[x] = false;
-      continue;
-    }
-    ident[x] = cnt[x] == span;
-    for (size_t i = 0; i < span && ident[x]; i++) ident[x] = map[x][i] == i;
-    k++;
+    k += want[x];
   }
-  if (k < 2) return GM_OK;  // not worth a shared plan
-  for (int x = 0; x < 3; x++) {
-    if (!want[x]) continue;
-    pk->wshare[x] = true;
-    if (ident[x]) continue;
-    if (hipMalloc(&pk->wmap[x], 4 * span) != hipSuccess) {
-      set_error("pk upload: hipMalloc of the wire map failed");
-      return GM_ERR_OOM;
-    }
-    GM_HIP(hipMemcpy(pk->wmap[x], map[x].data(), 4 * span, hipMemcpyHostToDevice));
-  }
-  pk->preW = pw;
-  (void)ctx;
-  return GM_OK;
+  if (k < 2)
+    for (int x = 0; x < 3; x++) want[x] = false;  // not worth a shared plan
 }
+
+namespace {
+// Wire-indexed copy of a compacted internal point array (and its window
+// copies): dst[w * span + i] = src[w * cnt + map[i]], infinity (all zero)
+// where wire i has no point.  q = 16-byte chunks per point.
+__global__ void k_expand_points(const uint4* __restrict__ src, size_t cnt, const uint32_t* __restrict__ map,
+                                size_t span, size_t total, uint32_t q, uint4* __restrict__ dst) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const size_t p = t / q, k = t - p * q;
+  const size_t w = p / span, i = p - w * span;
+  const uint32_t m = map[i];
+  dst[t] = m == MSM_SKIP ? make_uint4(0, 0, 0, 0) : src[((size_t)w * cnt + m) * q + k];
+}
+}  // namespace
 
 int prepare_points_into(gm_ctx* ctx, int curve, bool g2, const void* gnark_dev, size_t count,
                         const MsmPrecomp* pre, void* dst) {
@@ -244,21 +206,31 @@ int pk_upload_ranges(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsigned f
     for (auto* v : {&ia, &ib, &ik})
       for (auto& x : *v) x -= (x >= lo ? (uint32_t)lo : x);  // entries outside the slice are never read
   }
-  // window geometry: arrays that may share the wire plan take the plan's
-  // (chosen for the wire span), the others their own
-  bool wsh[3];
-  wire_plan_choice(pk->whi - pk->wlo, pk->nbA, pk->nbB, pk->nbK, wsh);
+  // Shared wire plan: arrays covering (nearly) every wire of the span are
+  // stored wire-indexed (expanded, infinity where a wire has no point), so one
+  // plan over the wires addresses all of them directly; window geometry and
+  // stride are the plan's.  The others keep their own compacted layout.
+  const size_t span = pk->whi - pk->wlo;
+  std::vector<uint32_t> wmap[3];
+  {
+    const uint32_t* idx[3] = {ia.data() + rg.loA, ib.data() + rg.loB, ik.data() + rg.loK};
+    const size_t cnt[3] = {pk->nbA, pk->nbB, pk->nbK};
+    wire_plan_choice(span, pk->nbA, pk->nbB, pk->nbK, pk->wshare);
+    wire_plan_maps(span, idx, cnt, pk->wshare, wmap);
+  }
   if (pk->precomp) {
-    const MsmPrecomp pw = msm_choose_precomp(pk->whi - pk->wlo, frbits);
+    const MsmPrecomp pw = msm_choose_precomp(span, frbits);
     auto geom = [&](size_t cnt, bool shared) {
       MsmPrecomp p = shared ? pw : msm_choose_precomp(cnt, frbits);
-      p.stride = cnt;
+      p.stride = shared ? span : cnt;
       return p;
     };
-    pk->preA = geom(pk->nbA, wsh[0]);
-    pk->preB = geom(pk->nbB, wsh[1]);
-    pk->preK = geom(pk->nbK, wsh[2]);
+    pk->preA = geom(pk->nbA, pk->wshare[0]);
+    pk->preB = geom(pk->nbB, pk->wshare[1]);
+    pk->preK = geom(pk->nbK, pk->wshare[2]);
     pk->preZ = msm_choose_precomp(pk->nbZ, frbits);
+    pk->preW = pw;
+    pk->preW.stride = span;
   }
   const size_t g1b = 2 * fp_bytes(curve), g2b = 4 * fp_bytes(curve);
   auto up = [&](const void* src, size_t bytes, void** dst) -> int {
@@ -278,7 +250,9 @@ int pk_upload_ranges(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsigned f
   };
   // gnark-layout points -> device-internal layout, once (plus the W-1
   // window-shifted copies with GM_PK_PRECOMPUTE, msm_precompute_points)
-  auto up_pts = [&](int which, const void* hsrc, size_t count, bool g2, const MsmPrecomp& pre, void** dst) -> int {
+  // emap: wire map of an expanded (shared-plan) array, else null
+  auto up_compact = [&](int which, const void* hsrc, size_t count, bool g2, const MsmPrecomp& pre,
+                        void** dst) -> int {
     const size_t copies = pk->precomp ? pre.W : 1;
     hipError_t e = hipMalloc(dst, internal_point_bytes(curve, g2) * (count ? count * copies : 1));
     if (e != hipSuccess) {
@@ -297,17 +271,46 @@ int pk_upload_ranges(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsigned f
     hipFree(tmp);
     return r;
   };
+  auto up_pts = [&](int which, const void* hsrc, size_t count, bool g2, const MsmPrecomp& pre, void** dst,
+                    const std::vector<uint32_t>* emap) -> int {
+    if (!emap) return up_compact(which, hsrc, count, g2, pre, dst);
+    MsmPrecomp pc = pre;  // compacted first (stride = count), then expanded to the span
+    pc.stride = count;
+    void* tmp = nullptr;
+    int r = up_compact(which, hsrc, count, g2, pc, &tmp);
+    const size_t copies = pk->precomp ? pre.W : 1;
+    const size_t ipb = internal_point_bytes(curve, g2), total = span * copies * (ipb / 16);
+    void* dmap = nullptr;
+    if (r == GM_OK && (hipMalloc(dst, ipb * (span ? span * copies : 1)) != hipSuccess ||
+                       hipMalloc(&dmap, 4 * (span ? span : 1)) != hipSuccess)) {
+      set_error("pk upload: hipMalloc of an expanded array failed");
+      r = GM_ERR_OOM;
+    }
+    if (r == GM_OK && span) {
+      if (hipMemcpy(dmap, emap->data(), 4 * span, hipMemcpyHostToDevice) != hipSuccess) r = GM_ERR_DEVICE;
+      if (r == GM_OK)
+        hipLaunchKernelGGL(k_expand_points, dim3(blocks_for(total, 256)), dim3(256), 0, ctx->stream,
+                           (const uint4*)tmp, count, (const uint32_t*)dmap, span, total, (uint32_t)(ipb / 16),
+                           (uint4*)*dst);
+      if (r == GM_OK && (hipGetLastError() != hipSuccess || hipStreamSynchronize(ctx->stream) != hipSuccess))
+        r = GM_ERR_DEVICE;
+      if (r) set_error("pk upload: expanding a point array failed");
+    }
+    if (tmp) hipFree(tmp);
+    if (dmap) hipFree(dmap);
+    return r;
+  };
+  auto em = [&](int x) { return pk->wshare[x] ? &wmap[x] : nullptr; };
   int rc;
-  if ((rc = up_pts(PK_A, h->g1_A, pk->nbA, false, pk->preA, &pk->A)) ||
-      (rc = up_pts(PK_B, h->g1_B, pk->nbB, false, pk->preB, &pk->B)) ||
-      (rc = up_pts(PK_Z, h->g1_Z, pk->nbZ, false, pk->preZ, &pk->Z)) ||
-      (rc = up_pts(PK_K, h->g1_K, pk->nbK, false, pk->preK, &pk->K)) ||
-      (rc = up_pts(PK_B2, h->g2_B, pk->nbB, true, pk->preB, &pk->B2)))
+  if ((rc = up_pts(PK_A, h->g1_A, pk->nbA, false, pk->preA, &pk->A, em(0))) ||
+      (rc = up_pts(PK_B, h->g1_B, pk->nbB, false, pk->preB, &pk->B, em(1))) ||
+      (rc = up_pts(PK_Z, h->g1_Z, pk->nbZ, false, pk->preZ, &pk->Z, nullptr)) ||
+      (rc = up_pts(PK_K, h->g1_K, pk->nbK, false, pk->preK, &pk->K, em(2))) ||
+      (rc = up_pts(PK_B2, h->g2_B, pk->nbB, true, pk->preB, &pk->B2, em(1))))
     return fail(rc);
   if ((rc = up(ia.data() + rg.loA, 4 * pk->nbA, &pk->idxA)) || (rc = up(ib.data() + rg.loB, 4 * pk->nbB, &pk->idxB)) ||
       (rc = up(ik.data() + rg.loK, 4 * pk->nbK, &pk->idxK)))
     return fail(rc);
-  if ((rc = pk_setup_wire_plan(ctx, pk, ia.data() + rg.loA, ib.data() + rg.loB, ik.data() + rg.loK))) return fail(rc);
   auto cp = [](std::vector<uint8_t>& v, const void* s, size_t b) {
     v.resize(b);
     memcpy(v.data(), s, b);
@@ -389,14 +392,30 @@ struct DeviceH : HSource {
   const gm_r1cs* r1 = nullptr;  // set: a, b, c evaluated from `wires` first
   const void* wires = nullptr;
   EventPair ev;  // a: inputs ready (main stream), b: h ready
+  bool launched = false;
   DeviceH(gm_ctx* x, gm_g16_pk* k, void* a_, void* b_, void* c_, size_t n_) : ctx(x), pk(k), a(a_), b(b_), c(c_), nc(n_) {}
+  // computeH is queued at the first poll(), i.e. after the shared wire plan's
+  // digits / sort (g16_sums_t polls once the plan is queued) and ordered after
+  // it: the LDS-heavy sort passes and NTT passes slow each other down (r03
+  // timeline: k_msm_s2_local 1.2 -> 14.5 ms beside the NTT) while the
+  // VALU-bound accumulation shares the chip with them at no extra cost.
+  // GM_G16_H_AFTER_PLAN=0 queues it at once (A/B).
   int start() {
     int rc;
     if ((rc = ev.create())) return rc;
+    static const bool after_plan = !getenv("GM_G16_H_AFTER_PLAN") || atoi(getenv("GM_G16_H_AFTER_PLAN")) != 0;
+    return after_plan ? GM_OK : launch();
+  }
+  int launch() {
+    if (launched) return GM_OK;
+    launched = true;
     GM_HIP(hipEventRecord(ev.a, ctx->stream));
     return launch_compute_h<C>(ctx, a, b, c, nc, pk->n, ev.a, ev.b, r1, wires);
   }
+  int poll() override { return launch(); }
   int z_scalars(const void** zs) override {
+    int rc;
+    if ((rc = launch())) return rc;
     GM_HIP(hipStreamWaitEvent(ctx->stream, ev.b, 0));
     *zs = (const char*)a + 32 * pk->zlo;
     return GM_OK;
@@ -733,9 +752,8 @@ int g16_sums_t(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, HSource& hs, G
     }
   }
   GM_HIP(hipGetLastError());
-  // The shared wire plan (pk_setup_wire_plan): ONE digit / sort plan over the
-  // wire slice serves the A, B, B2 and K MSMs of arrays that cover it; an array
-  // with a wire map reads the plan's entries translated to its own points.
+  // The shared wire plan: ONE digit / sort plan over the wire slice serves the
+  // A, B, B2 and K MSMs of the wire-indexed arrays (pk_upload_ranges).
   MsmPlan planX[3];
   bool have[3] = {false, false, false};
   if (pk->wshare[0] || pk->wshare[1] || pk->wshare[2]) {
@@ -744,18 +762,8 @@ int g16_sums_t(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, HSource& hs, G
     if ((rc = msm_plan<C>(ctx, arena, wires_dev, pk->whi - pk->wlo, pW, planW))) return rc;
     for (int x = 0; x < 3; x++) {
       if (!pk->wshare[x]) continue;
-      planX[x] = planW;
-      planX[x].npts = pX[x] ? (size_t)pX[x]->W * pX[x]->stride : nX[x];
+      planX[x] = planW;  // the array is wire-indexed: the plan's entries address it directly
       have[x] = true;
-      if (!pk->wmap[x] || planW.n == 0) continue;
-      ProfScope ps(ctx, "map_plan_vals");
-      DevBuf mv;
-      if ((rc = mv.alloc(arena, sizeof(uint32_t) * planW.M))) return rc;
-      hipLaunchKernelGGL(k_map_plan_vals, dim3(blocks_for(planW.M, 256)), dim3(256), 0, st, planW.vals,
-                         planW.offsets, planW.total, planW.M, (const uint32_t*)pk->wmap[x],
-                         pW ? (uint32_t)pW->stride : 0u, pX[x] ? (uint32_t)pX[x]->stride : 0u, mv.as<uint32_t>());
-      GM_HIP(hipGetLastError());
-      planX[x].vals = mv.as<uint32_t>();
     }
   }
   // launch array x's MSM into `slot`: on the shared plan, or plan + launch

@@ -20,12 +20,12 @@ struct gm_g16_pk {
   gm::MsmPrecomp preA, preB, preZ, preK;  // layouts (B and B2 share preB)
   std::vector<uint8_t> alpha, beta, delta, beta2, delta2;  // host affine
   // Shared wire plan: when the A, B (+ B2) and K arrays each cover (nearly)
-  // every wire of [wlo, whi), their MSMs read ONE digit / sort plan over the
-  // wire slice instead of one per array (g16_sums_t).  wmap[X][i] = array X's
-  // point index for wire wlo + i, or MSM_SKIP; nullptr = identity.
-  bool wshare[3] = {false, false, false};  // A, B, K
-  void* wmap[3] = {nullptr, nullptr, nullptr};
-  gm::MsmPrecomp preW;  // the wire plan's geometry (precomp: same c / W / narrow as the shared arrays)
+  // every wire of [wlo, whi), they are stored wire-indexed -- point i of a copy
+  // belongs to wire wlo + i, infinity where the wire has none -- and their MSMs
+  // read ONE digit / sort plan over the wire slice instead of one per array
+  // (g16_sums_t).  The compaction maps idxX stay as they are.
+  bool wshare[3] = {false, false, false};  // A, B (and B2), K
+  gm::MsmPrecomp preW;  // the wire plan's geometry (precomp: c / W / narrow of the shared arrays, stride = span)
 };
 
 namespace gm {
@@ -52,9 +52,23 @@ int prepare_points_into(gm_ctx* ctx, int curve, bool g2, const void* gnark_dev, 
 // (upload and cache load decide alike): each covers >= 31/32 of the `span`
 // wires, and at least two of them do.  GM_G16_WIRE_PLAN=0 disables it.
 void wire_plan_choice(size_t span, size_t nbA, size_t nbB, size_t nbK, bool out[3]);
-// Builds pk's wire maps from the key's local compaction maps (wire - wlo per
-// point of A, B, K; host memory) and sets pk->wshare / wmap / preW.
-int pk_setup_wire_plan(gm_ctx* ctx, gm_g16_pk* pk, const uint32_t* ia, const uint32_t* ib, const uint32_t* ik);
+// Wire maps of the chosen arrays from their local compaction maps (wire - wlo
+// per point): map[x][i] = point index of wire i or MSM_SKIP.  An array whose
+// map would repeat a wire drops out; fewer than two left: none shares.
+void wire_plan_maps(size_t span, const uint32_t* const idx[3], const size_t cnt[3], bool want[3],
+                    std::vector<uint32_t> map[3]);
+// points per window copy of array which (PK_A..PK_B2): the wire span when the
+// array is wire-indexed (shared plan), else its own count
+inline size_t pk_array_points(const gm_g16_pk* pk, int which) {
+  const size_t span = pk->whi - pk->wlo;
+  switch (which) {
+    case 0: return pk->wshare[0] ? span : pk->nbA;
+    case 1:
+    case 4: return pk->wshare[1] ? span : pk->nbB;
+    case 2: return pk->nbZ;
+    default: return pk->wshare[2] ? span : pk->nbK;
+  }
+}
 // a, b, c = <L_i, w>, <R_i, w>, <O_i, w> of a device-resident R1CS (r1cs.hip),
 // queued on ctx->stream
 int r1cs_eval_device(gm_ctx* ctx, const gm_r1cs* r, const void* wires_dev, void* a, void* b, void* c);

@@ -97,9 +97,10 @@ inline bool msm_glv_g2_enabled() {
   static const bool on = !(getenv("GM_MSM_GLV_G2") && getenv("GM_MSM_GLV_G2")[0] == '0');
   return on;
 }
-// GLV for an MSM on ctx: the context's setting (gm_set_msm_glv) or, by
-// default, the environment's (GM_MSM_GLV / GM_MSM_GLV_G2)
-bool msm_glv_on(const gm_ctx* ctx, bool g2);
+// GLV for an MSM of n points on ctx: the context's setting (gm_set_msm_glv)
+// or, by default, the environment's (GM_MSM_GLV / GM_MSM_GLV_G2) for n up to
+// 2^21 (GM_MSM_GLV_MAXLOG)
+bool msm_glv_on(const gm_ctx* ctx, bool g2, size_t n);
 template <class C, bool G2>
 int msm_run(gm_ctx* ctx, const MsmPlan& plan, const void* points_internal,
             typename GroupSel<C, G2>::HF (&jac_out)[3]);

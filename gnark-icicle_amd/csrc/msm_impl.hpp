@@ -1218,7 +1218,7 @@ int msm_device_launch(gm_ctx* ctx, Arena& arena, const void* scalars_dev, const 
       set_error("msm: a precomputed point set must be device-internal");
       return GM_ERR_INVALID;
     }
-    glv = Glv<C>::ok && msm_glv_on(ctx, G2);
+    glv = Glv<C>::ok && msm_glv_on(ctx, G2, n);
     if ((rc = ipts.alloc(arena, 2 * Coord<DF>::WORDS * sizeof(uint32_t) * n * (glv ? 2 : 1)))) return rc;
     ProfScope ps(ctx, "msm_convert_points");
     if constexpr (Glv<C>::ok) {

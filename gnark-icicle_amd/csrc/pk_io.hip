@@ -143,7 +143,7 @@ void shard_range(size_t n, int rank, int world, size_t* lo, size_t* hi) {
 
 // ---- device-layout cache ---------------------------------------------------
 constexpr char CACHE_MAGIC[8] = {'G', 'M', 'P', 'K', 'C', 'A', 'C', 'H'};
-constexpr uint32_t CACHE_VERSION = 2;
+constexpr uint32_t CACHE_VERSION = 3;
 // Device-layout fingerprint: the internal point form (radix-2^29 Montgomery
 // limbs packed in gnark's word layout) and the precomputed-copy rule
 // (PRECOMP_LAYOUT, msm.hpp).  A cache written by a build with another layout is
@@ -153,7 +153,7 @@ constexpr uint32_t CACHE_LAYOUT = (uint32_t(RADIX) << 24) | (uint32_t(PRECOMP_LA
 struct CacheHeader {
   char magic[8];
   uint32_t version, curve;
-  uint32_t layout, reserved;
+  uint32_t layout, wshare;  // wshare: bit x = array x (A, B, K) wire-indexed (shared wire plan)
   uint64_t n, nb_wires, nb_public, nbA, nbB, nbK, zlo, nbZ, wlo, whi, precomp;
   uint32_t pre_c[4], pre_W[4];
   uint64_t pre_stride[4];
@@ -173,9 +173,14 @@ int check_cache_header(const CacheHeader& h) {
   if (h.wlo > h.whi || h.whi > h.nb_wires) return bad("wire slice");
   if (h.nbA > h.nb_wires || h.nbB > h.nb_wires || h.nbK > h.nb_wires) return bad("array lengths");
   if (h.precomp > 1) return bad("precompute flag");
+  if (h.wshare > 7) return bad("shared-plan flags");
+  const uint64_t span = h.whi - h.wlo;
+  if (((h.wshare & 1) && h.nbA > span) || ((h.wshare & 2) && h.nbB > span) || ((h.wshare & 4) && h.nbK > span))
+    return bad("wire-indexed array longer than its wire span");
   if (h.precomp) {
     const int frbits = h.curve == GM_BN254 ? CurveBN254::FR_BITS : CurveBLS12377::FR_BITS;
-    const uint64_t cnt[4] = {h.nbA, h.nbB, h.nbZ, h.nbK};
+    const uint64_t cnt[4] = {(h.wshare & 1) ? span : h.nbA, (h.wshare & 2) ? span : h.nbB, h.nbZ,
+                             (h.wshare & 4) ? span : h.nbK};
     for (int i = 0; i < 4; i++) {
       if (h.pre_c[i] < 1 || h.pre_c[i] > 30 || h.pre_W[i] < 1 ||
           (uint64_t)h.pre_c[i] * h.pre_W[i] < (uint64_t)frbits + 1)
@@ -190,11 +195,11 @@ size_t array_bytes(const gm_g16_pk* pk, int which) {
   const size_t g1 = internal_point_bytes(pk->curve, false), g2 = internal_point_bytes(pk->curve, true);
   auto copies = [&](const MsmPrecomp& p) { return pk->precomp ? (size_t)p.W : size_t(1); };
   switch (which) {
-    case PK_A: return g1 * pk->nbA * copies(pk->preA);
-    case PK_B: return g1 * pk->nbB * copies(pk->preB);
+    case PK_A: return g1 * pk_array_points(pk, PK_A) * copies(pk->preA);
+    case PK_B: return g1 * pk_array_points(pk, PK_B) * copies(pk->preB);
     case PK_Z: return g1 * pk->nbZ * copies(pk->preZ);
-    case PK_K: return g1 * pk->nbK * copies(pk->preK);
-    case PK_B2: return g2 * pk->nbB * copies(pk->preB);
+    case PK_K: return g1 * pk_array_points(pk, PK_K) * copies(pk->preK);
+    case PK_B2: return g2 * pk_array_points(pk, PK_B2) * copies(pk->preB);
     case 5: return 4 * pk->nbA;
     case 6: return 4 * pk->nbB;
     default: return 4 * pk->nbK;
@@ -325,6 +330,7 @@ int gm_g16_pk_save_cache(gm_ctx* ctx, const gm_g16_pk* pk, int fd) {
   memcpy(h.magic, CACHE_MAGIC, 8);
   h.version = CACHE_VERSION;
   h.layout = CACHE_LAYOUT;
+  h.wshare = (pk->wshare[0] ? 1u : 0u) | (pk->wshare[1] ? 2u : 0u) | (pk->wshare[2] ? 4u : 0u);
   h.curve = (uint32_t)pk->curve;
   h.n = pk->n;
   h.nb_wires = pk->nb_wires;
@@ -405,6 +411,18 @@ int gm_g16_pk_load_cache(gm_ctx* ctx, int fd, gm_g16_pk** out) {
     pres[i]->narrow = precomp_narrow(h.pre_c[i], h.pre_W[i], frbits);  // layout 2 (CACHE_LAYOUT)
     pres[i]->stride = h.pre_stride[i];
   }
+  for (int x = 0; x < 3; x++) pk->wshare[x] = (h.wshare >> x) & 1;
+  if (pk->precomp && h.wshare) {
+    pk->preW = msm_choose_precomp(pk->whi - pk->wlo, frbits);
+    pk->preW.stride = pk->whi - pk->wlo;
+    const MsmPrecomp* shared[3] = {&pk->preA, &pk->preB, &pk->preK};
+    for (int x = 0; x < 3; x++)
+      if (pk->wshare[x] && (shared[x]->c != pk->preW.c || shared[x]->W != pk->preW.W ||
+                            shared[x]->narrow != pk->preW.narrow || shared[x]->stride != pk->preW.stride)) {
+        set_error("pk cache: wire-indexed array without the wire plan's window geometry");
+        return fail(GM_ERR_INVALID);
+      }
+  }
   const size_t g1b = 2 * fp_bytes(pk->curve), g2b = 4 * fp_bytes(pk->curve);
   for (auto* v : {&pk->alpha, &pk->beta, &pk->delta}) v->resize(g1b);
   for (auto* v : {&pk->beta2, &pk->delta2}) v->resize(g2b);
@@ -448,18 +466,6 @@ int gm_g16_pk_load_cache(gm_ctx* ctx, int fd, gm_g16_pk** out) {
     }
   }
   if (hipStreamSynchronize(ctx->stream) != hipSuccess) return fail(GM_ERR_DEVICE);
-  // the shared wire plan is derived state: rebuilt from the compaction maps
-  {
-    std::vector<uint32_t> ix[3];
-    void* src[3] = {pk->idxA, pk->idxB, pk->idxK};
-    const size_t cnt[3] = {pk->nbA, pk->nbB, pk->nbK};
-    for (int x = 0; x < 3; x++) {
-      ix[x].resize(cnt[x] ? cnt[x] : 1);
-      if (cnt[x] && hipMemcpy(ix[x].data(), src[x], 4 * cnt[x], hipMemcpyDeviceToHost) != hipSuccess)
-        return fail(GM_ERR_DEVICE);
-    }
-    if ((rc = pk_setup_wire_plan(ctx, pk, ix[0].data(), ix[1].data(), ix[2].data()))) return fail(rc);
-  }
   *out = pk;
   return GM_OK;
 }

@@ -62,9 +62,9 @@ int gm_profile_dump(gm_ctx* ctx, char* buf, size_t cap);
 /* Test/tuning knob: force the MSM window size c (0 = automatic). */
 int gm_set_msm_window(gm_ctx* ctx, int c);
 /* GLV split (k = k1 + k2 lambda over P_i and phi(P_i), BN254 and BLS12-377) of
- * MSMs over gnark-layout points: mode 1 on, 0 off, -1 default (on unless
- * GM_MSM_GLV=0; G2 also unless GM_MSM_GLV_G2=0).  Tuning / A-B knob; results
- * are identical either way. */
+ * MSMs over gnark-layout points: mode 1 on, 0 off, -1 default (on up to 2^21
+ * points unless GM_MSM_GLV=0; G2 also unless GM_MSM_GLV_G2=0).  Tuning / A-B
+ * knob; results are identical either way. */
 int gm_set_msm_glv(gm_ctx* ctx, int mode);
 
 /* ---- memory (iciclegnark CopyToDevice / CopyPointsToDevice /

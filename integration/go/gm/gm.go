@@ -222,6 +222,69 @@ func (k *G16Key) Prove(wires, a, b, c unsafe.Pointer, nbConstraints int, r, s, a
 	return nil
 }
 
+// R1CS is a constraint system resident on device 0 (gm_r1cs_upload): proofs then
+// need the wires alone (ProveR1CS), a / b / c are evaluated on the GPU.
+type R1CS struct{ h *C.gm_r1cs }
+
+// R1CSConst marks a constant term's wire id (constraint.Term.IsConstant).
+const R1CSConst = C.GM_R1CS_CONST
+
+// UploadR1CS uploads the CSR form of r1cs.GetR1Cs() (per matrix L, R, O: row
+// pointers, coefficient ids, wire ids) and the CoeffTable (coeffs points at
+// the first fr.Element of r1cs.Coefficients).
+func UploadR1CS(curve int, nbConstraints, nbWires int, rowptr, cid, vid [3][]uint32, coeffs unsafe.Pointer,
+	ncoeffs int) (*R1CS, error) {
+	ctx, err := Ctx()
+	if err != nil {
+		return nil, err
+	}
+	// the three pointer arrays live in C memory: a Go array of Go pointers
+	// would itself need every element pinned (§2.1 of INTEGRATION.md)
+	arr := func(v [3][]uint32) **C.uint32_t {
+		p := (*[3]*C.uint32_t)(C.malloc(C.size_t(3 * unsafe.Sizeof(uintptr(0)))))
+		for m := 0; m < 3; m++ {
+			p[m] = nil
+			if len(v[m]) > 0 {
+				p[m] = (*C.uint32_t)(unsafe.Pointer(&v[m][0]))
+			}
+		}
+		return &p[0]
+	}
+	var pin runtime.Pinner
+	defer pin.Unpin()
+	for m := 0; m < 3; m++ {
+		for _, v := range [][]uint32{rowptr[m], cid[m], vid[m]} {
+			if len(v) > 0 {
+				pin.Pin(&v[0])
+			}
+		}
+	}
+	rp, ci, vi := arr(rowptr), arr(cid), arr(vid)
+	defer C.free(unsafe.Pointer(rp))
+	defer C.free(unsafe.Pointer(ci))
+	defer C.free(unsafe.Pointer(vi))
+	r := &R1CS{}
+	if rc := C.gm_r1cs_upload(ctx, C.int(curve), C.size_t(nbConstraints), C.size_t(nbWires), rp, ci, vi, coeffs,
+		C.size_t(ncoeffs), &r.h); rc != C.GM_OK {
+		return nil, lastErr("gm_r1cs_upload", rc)
+	}
+	return r, nil
+}
+
+// Free releases the device copy.
+func (r *R1CS) Free() { C.gm_r1cs_free(ctx0, r.h) }
+
+// ProveR1CS is Prove with the wires as the only host input (single-device keys).
+func (k *G16Key) ProveR1CS(r1 *R1CS, wires unsafe.Pointer, r, s, ar, bs, krs unsafe.Pointer) error {
+	if k.single == nil {
+		return errors.New("gnark_mi355x: ProveR1CS needs a single-device key")
+	}
+	if rc := C.gm_g16_prove_r1cs(ctx0, k.single, r1.h, wires, r, s, ar, bs, krs); rc != C.GM_OK {
+		return lastErr("gm_g16_prove_r1cs", rc)
+	}
+	return nil
+}
+
 // UploadG16KeyDump streams the five point slices of a WriteDump file
 // (marshal.go:389-456) from f, starting at byte offset (where ReadDump,
 // marshal.go:511, starts reading them), straight into device buffers; k holds

@@ -19,6 +19,7 @@ package icicle_bn254
 import (
 	"fmt"
 	"math/big"
+	"os"
 	"unsafe"
 
 	"github.com/consensys/gnark-crypto/ecc"
@@ -101,7 +102,36 @@ func (pk *ProvingKey) setupDevicePointers(r1cs *cs.R1CS) error {
 		return err
 	}
 	pk.deviceInfo = &deviceInfo{key: key}
+	// the constraint system too (one GPU): proofs then send the wires alone
+	if gm.NbDevices() == 1 && os.Getenv("GNARK_MI355X_R1CS") != "0" {
+		if pk.deviceInfo.r1, err = uploadR1CS(r1cs); err != nil {
+			return err
+		}
+	}
 	return nil
+}
+
+// uploadR1CS hands r1cs.GetR1Cs() (constraint.R1C: L, R, O linear expressions
+// of constraint.Term{CID, VID}; VID = MaxUint32 for a constant term, as
+// GM_R1CS_CONST) and the CoeffTable to gm_r1cs_upload.
+func uploadR1CS(r1cs *cs.R1CS) (*gm.R1CS, error) {
+	rows := r1cs.GetR1Cs()
+	var rowptr, cid, vid [3][]uint32
+	for m := 0; m < 3; m++ {
+		rowptr[m] = make([]uint32, 1, len(rows)+1)
+	}
+	for i := range rows {
+		for m, l := range [3]constraint.LinearExpression{rows[i].L, rows[i].R, rows[i].O} {
+			for _, t := range l {
+				cid[m] = append(cid[m], t.CID)
+				vid[m] = append(vid[m], t.VID)
+			}
+			rowptr[m] = append(rowptr[m], uint32(len(cid[m])))
+		}
+	}
+	internal, secret, public := r1cs.GetNbVariables() // constraint/core.go:214
+	return gm.UploadR1CS(gm.BN254, len(rows), internal+secret+public, rowptr, cid, vid,
+		unsafe.Pointer(&r1cs.Coefficients[0]), len(r1cs.Coefficients))
 }
 
 // bsb22Hint is the BSB22 commitment hint of prove.go:82-109: it commits to the
@@ -210,6 +240,14 @@ func Prove(r1cs *cs.R1CS, pk *ProvingKey, fullWitness witness.Witness, opts ...b
 		return nil, err
 	}
 
+	if pk.deviceInfo.r1 != nil { // a, b, c come from the resident R1CS
+		if err := pk.deviceInfo.key.ProveR1CS(pk.deviceInfo.r1, unsafe.Pointer(&w[0]), unsafe.Pointer(&r),
+			unsafe.Pointer(&s), unsafe.Pointer(&proof.Ar), unsafe.Pointer(&proof.Bs), unsafe.Pointer(&proof.Krs)); err != nil {
+			return nil, err
+		}
+		log.Debug().Msg("prover done")
+		return proof, nil
+	}
 	nbCons := len(solution.A)
 	if err := pk.deviceInfo.key.Prove(unsafe.Pointer(&w[0]), unsafe.Pointer(&solution.A[0]),
 		unsafe.Pointer(&solution.B[0]), unsafe.Pointer(&solution.C[0]), nbCons,

@@ -24,6 +24,7 @@ import (
 
 type deviceInfo struct {
 	key *gm.G16Key
+	r1  *gm.R1CS // resident constraint system (nil: a, b, c sent per proof)
 }
 
 type ProvingKey struct {
@@ -44,6 +45,9 @@ func DummySetup(r1cs *cs.R1CS, pk *ProvingKey) error {
 func (pk *ProvingKey) FreeDevice() {
 	if pk.deviceInfo != nil {
 		pk.deviceInfo.key.Free()
+		if pk.deviceInfo.r1 != nil {
+			pk.deviceInfo.r1.Free()
+		}
 		pk.deviceInfo = nil
 	}
 }
