@@ -347,16 +347,17 @@ template <class C>
 int launch_compute_h(gm_ctx* ctx, void* a, void* b, void* c, size_t nc, size_t n, hipEvent_t wait_for,
                      hipEvent_t done, const gm_r1cs* r1 = nullptr, const void* wires = nullptr) {
   static const bool overlap = !getenv("GM_G16_OVERLAP") || atoi(getenv("GM_G16_OVERLAP")) != 0;
+  // n == 0: only the R1CS evaluation (no done event); computeH follows later
   auto body = [&]() -> int {
     int rc;
     if (r1 && (rc = r1cs_eval_device(ctx, r1, wires, a, b, c))) return rc;
-    return compute_h_device<C>(ctx, a, b, c, nc, n);
+    return n ? compute_h_device<C>(ctx, a, b, c, nc, n) : GM_OK;
   };
   if (!overlap) {
     if (wait_for) GM_HIP(hipStreamWaitEvent(ctx->stream, wait_for, 0));
     int rc = body();
     if (rc) return rc;
-    GM_HIP(hipEventRecord(done, ctx->stream));
+    if (done) GM_HIP(hipEventRecord(done, ctx->stream));
     return GM_OK;
   }
   if (wait_for) GM_HIP(hipStreamWaitEvent(ctx->aux, wait_for, 0));
@@ -365,7 +366,7 @@ int launch_compute_h(gm_ctx* ctx, void* a, void* b, void* c, size_t nc, size_t n
   int rc = body();
   ctx->stream = main;
   if (rc) return rc;
-  GM_HIP(hipEventRecord(done, ctx->aux));
+  if (done) GM_HIP(hipEventRecord(done, ctx->aux));
   return GM_OK;
 }
 
@@ -399,12 +400,21 @@ struct DeviceH : HSource {
   // it: the LDS-heavy sort passes and NTT passes slow each other down (r03
   // timeline: k_msm_s2_local 1.2 -> 14.5 ms beside the NTT) while the
   // VALU-bound accumulation shares the chip with them at no extra cost.
-  // GM_G16_H_AFTER_PLAN=0 queues it at once (A/B).
+  // GM_G16_H_AFTER_PLAN=0 queues it at once (A/B).  The R1CS evaluation (a
+  // latency-bound gather, 0.65 ms alone at 2^24 but 18 ms beside the
+  // accumulation) is not deferred: it runs on the auxiliary stream next to the
+  // digit pass.
   int start() {
     int rc;
     if ((rc = ev.create())) return rc;
     static const bool after_plan = !getenv("GM_G16_H_AFTER_PLAN") || atoi(getenv("GM_G16_H_AFTER_PLAN")) != 0;
-    return after_plan ? GM_OK : launch();
+    if (!after_plan) return launch();
+    if (r1) {
+      GM_HIP(hipEventRecord(ev.a, ctx->stream));
+      if ((rc = launch_compute_h<C>(ctx, a, b, c, nc, 0, ev.a, nullptr, r1, wires))) return rc;
+      r1 = nullptr;
+    }
+    return GM_OK;
   }
   int launch() {
     if (launched) return GM_OK;

@@ -428,18 +428,6 @@ GM_DEV PackedPt<PW> load_packed_pt(const uint32_t* __restrict__ src) {
   return r;
 }
 
-// point idx, or the all-zero (infinity) point for a skipped entry (MSM_SKIP)
-template <int PW>
-GM_DEV PackedPt<PW> load_packed_pt_or_inf(const uint32_t* __restrict__ points, uint32_t idx) {
-  if (idx == MSM_SKIP) {
-    PackedPt<PW> z;
-#pragma unroll
-    for (int q = 0; q < PW; q++) z.w[q] = 0;
-    return z;
-  }
-  return load_packed_pt<PW>(points + (size_t)idx * PW);
-}
-
 // Load-balanced accumulation over the sorted entry list: thread t owns entries
 // [t*K, t*K+K).  A bucket whose whole range lies in the thread's slice is
 // written straight to `buckets`; the (at most two) buckets cut by the slice
@@ -500,12 +488,12 @@ GM_DEV void accum_seg_body(const uint32_t* __restrict__ points, uint32_t n,
   bool first = true;
   XYZZ<F> acc = xyzz_inf<F>();
   uint32_t idx = v & 0x7fffffffu;
-  if (idx >= n && idx != MSM_SKIP) {
+  if (idx >= n) {
     atomicOr(err, 2u);
     return;
   }
   constexpr int PW = 2 * Coord<F>::WORDS;  // u32 words per packed point
-  PackedPt<PW> P = load_packed_pt_or_inf<PW>(points, idx);
+  PackedPt<PW> P = load_packed_pt<PW>(points + (size_t)idx * PW);
   for (uint32_t q = start; q < end; q++) {
     const uint32_t k = keys[q];
     // prefetch the next point's words while this add runs
@@ -514,11 +502,11 @@ GM_DEV void accum_seg_body(const uint32_t* __restrict__ points, uint32_t n,
     if (PREFETCH && q + 1 < end) {
       vn = vals[q + 1];
       const uint32_t in = vn & 0x7fffffffu;
-      if (in >= n && in != MSM_SKIP) {
+      if (in >= n) {
         atomicOr(err, 2u);
         return;
       }
-      Pn = load_packed_pt_or_inf<PW>(points, in);
+      Pn = load_packed_pt<PW>(points + (size_t)in * PW);
     }
     if (k != cur) {
       accum_emit(cur, acc, first, false, start, end, t, offsets, buckets, part_first, part_last);
@@ -526,7 +514,7 @@ GM_DEV void accum_seg_body(const uint32_t* __restrict__ points, uint32_t n,
       acc = xyzz_inf<F>();
       cur = k;
     }
-    if (!PREFETCH) P = load_packed_pt_or_inf<PW>(points, v & 0x7fffffffu);
+    if (!PREFETCH) P = load_packed_pt<PW>(points + (size_t)(v & 0x7fffffffu) * PW);
     Affine<F> A = load_affine_packed<F>(P.w);
     if (v >> 31) A.y = fe_neg(A.y);
     LazyAcc<F>::add(acc, A);
@@ -535,7 +523,7 @@ GM_DEV void accum_seg_body(const uint32_t* __restrict__ points, uint32_t n,
       P = Pn;
     } else if (q + 1 < end) {
       v = vals[q + 1];
-      if ((v & 0x7fffffffu) >= n && (v & 0x7fffffffu) != MSM_SKIP) {
+      if ((v & 0x7fffffffu) >= n) {
         atomicOr(err, 2u);
         return;
       }

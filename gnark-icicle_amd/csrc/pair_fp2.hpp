@@ -11,7 +11,6 @@
 // All control flow that depends on values is made pair-uniform (pair_all).
 #pragma once
 #include "curve.hpp"
-#include "msm.hpp"
 
 namespace gm {
 
@@ -189,17 +188,6 @@ GM_DEV PairPt<P> pair_load_pt(const uint32_t* __restrict__ pt) {
   const int c = pair_odd() ? P::NG : 0;
   return {feg_load<P>(pt + c), feg_load<P>(pt + 2 * P::NG + c)};
 }
-// point idx, or the all-zero (infinity) point for a skipped entry (MSM_SKIP)
-template <class P>
-GM_DEV PairPt<P> pair_load_pt_or_inf(const uint32_t* __restrict__ points, uint32_t idx) {
-  if (idx == MSM_SKIP) {
-    PairPt<P> z;
-#pragma unroll
-    for (int i = 0; i < P::NG; i++) z.x.w[i] = z.y.w[i] = 0;
-    return z;
-  }
-  return pair_load_pt<P>(points + (size_t)idx * 4 * P::NG);
-}
 
 #ifndef GM_PAIR_WPE
 #define GM_PAIR_WPE 1  // no cap; per-TU override (msm_bls12377_g2.hip)
@@ -233,11 +221,11 @@ __global__ void __launch_bounds__(128) GM_PAIR_ATTR k_msm_accum_seg_pair(const u
   uint32_t cur = keys[start];
   bool first = true;
   PXYZZ<P> acc = pxyzz_inf<P>();
-  if ((v & 0x7fffffffu) >= n && (v & 0x7fffffffu) != MSM_SKIP) {
+  if ((v & 0x7fffffffu) >= n) {
     if (!pair_odd()) atomicOr(err, 2u);
     return;
   }
-  PairPt<P> pt = pair_load_pt_or_inf<P>(points, v & 0x7fffffffu);
+  PairPt<P> pt = pair_load_pt<P>(points + (size_t)(v & 0x7fffffffu) * 4 * P::NG);
   for (uint32_t q = start; q < end; q++) {
     const uint32_t k = keys[q];
     // prefetch the next point's components while this add runs
@@ -245,11 +233,11 @@ __global__ void __launch_bounds__(128) GM_PAIR_ATTR k_msm_accum_seg_pair(const u
     PairPt<P> ptn;
     if (q + 1 < end) {
       vn = vals[q + 1];
-      if ((vn & 0x7fffffffu) >= n && (vn & 0x7fffffffu) != MSM_SKIP) {
+      if ((vn & 0x7fffffffu) >= n) {
         if (!pair_odd()) atomicOr(err, 2u);
         return;
       }
-      ptn = pair_load_pt_or_inf<P>(points, vn & 0x7fffffffu);
+      ptn = pair_load_pt<P>(points + (size_t)(vn & 0x7fffffffu) * 4 * P::NG);
     }
     if (k != cur) {
       emit(cur, acc, first, false);

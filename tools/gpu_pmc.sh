@@ -21,6 +21,6 @@ for P in "$P1" "$P2"; do
     fi
   done
   echo "pass $k:$L"
-  timeout -s KILL 90 rocprofv3 --pmc $L --output-format csv -d gpurun_out/${T}_pmc$k -o pmc -- python3 tools/msm_only.py "$@" > gpurun_out/${T}_pmc$k.out 2>&1 || { tail -5 gpurun_out/${T}_pmc$k.out; exit 1; }
+  timeout -s KILL 90 rocprofv3 --pmc $L --output-format csv -d gpurun_out/${T}_pmc$k -o pmc -- python3 ${PROG:-tools/msm_only.py} "$@" > gpurun_out/${T}_pmc$k.out 2>&1 || { tail -5 gpurun_out/${T}_pmc$k.out; exit 1; }
 done
 python3 tools/pmc_summary.py gpurun_out/${T}_pmc1 gpurun_out/${T}_pmc2 > gpurun_out/${T}_pmc_summary.txt && cat gpurun_out/${T}_pmc_summary.txt
