@@ -109,28 +109,33 @@ GM_DEV void xyzz_add_aff(XYZZ<F>& a, const Affine<F>& p) {
   a.x = X3;
 }
 
-// Lazily reduced a += p for G1 buckets (see field.hpp "Lazily reduced
-// arithmetic").  Invariants on a: x < 8p, y < 4p, zz < 2p, zzz < 2p (canonical
-// values qualify); p canonical.  Every product below has inputs with
+// Lazily reduced a += (neg ? -p : p) for G1 buckets (see field.hpp "Lazily
+// reduced arithmetic").  Invariants on a: x < 8p, y < 4p, zz < 2p, zzz < 2p
+// (canonical values qualify); p canonical.  Every product below has inputs with
 // ab <= 100 p^2 (largest: P^2 with P < 10p).  zz is never a non-zero multiple
 // of p (zz * PP with PP != 0 mod p), so fe_is_zero(zz) still tests infinity.
+// The digit sign is applied to S2 = y zzz (carry-free 2p - S2) rather than to y,
+// and X3 = R^2 - PPP - 2Q takes one borrow chain (fe_sub2x_lz).
 template <class P>
-GM_DEV void xyzz_add_aff_lz(XYZZ<Fe<P>>& a, const Affine<Fe<P>>& p) {
+GM_DEV void xyzz_add_aff_lz(XYZZ<Fe<P>>& a, const Affine<Fe<P>>& p, bool neg) {
   static_assert(P::BITS + 7 <= RADIX * P::N, "lazy reduction needs R' > 128 p");
   using F = Fe<P>;
   if (aff_is_inf(p)) return;
   if (xyzz_is_inf(a)) {
     a.x = p.x;
-    a.y = p.y;
+    a.y = neg ? fe_neg(p.y) : p.y;
     a.zz = fe_one<P>();
     a.zzz = fe_one<P>();
     return;
   }
   F Pd = fe_sub_lz<8>(fe_mul_lz(p.x, a.zz), a.x);   // U2 - X1   < 10p
-  F R = fe_sub_lz<4>(fe_mul_lz(p.y, a.zzz), a.y);   // S2 - Y1   < 6p
+  // +-S2 - Y1 < 6p  (S2 = y zzz < 2p; 2p - S2 in (0, 2p])
+  F R = fe_sub_lz<4>(fe_cneg2p_cf(fe_mul_lz(p.y, a.zzz), neg), a.y);
   if (fe_is_zero_lz<10>(Pd)) {
     if (fe_is_zero_lz<6>(R)) {
-      a = xyzz_dbl_aff(p);
+      Affine<F> q = p;
+      if (neg) q.y = fe_neg(p.y);
+      a = xyzz_dbl_aff(q);
     } else {
       a = xyzz_inf<F>();
     }
@@ -141,7 +146,7 @@ GM_DEV void xyzz_add_aff_lz(XYZZ<Fe<P>>& a, const Affine<Fe<P>>& p) {
   a.zz = fe_mul_lz(a.zz, PP);
   F Q = fe_mul_lz(a.x, PP);                          // < 2p
   a.zzz = fe_mul_lz(a.zzz, PPP);
-  F X3 = fe_sub_lz<4>(fe_sub_lz<2>(fe_sqr_lz(R), PPP), fe_add_lz(Q, Q));  // < 8p
+  F X3 = fe_sub2x_lz<6>(fe_sqr_lz(R), PPP, Q);       // R^2 - PPP - 2Q + 6p < 8p
   // R (< 6p) * (Q - X3 + 8p < 10p) - Y1 (< 4p) * PPP (< 2p), one reduction:
   // < 60 p^2 / R' + 2p < 2.4p (x2 y2 = 8 p^2 < R' p as fe_mul2_redc needs)
   a.y = fe_mul2_redc(R, fe_sub_lz<8>(Q, X3), a.y, PPP, true);

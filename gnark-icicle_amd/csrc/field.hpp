@@ -448,6 +448,41 @@ GM_DEV void fe_reduce_k(Fe<P>& a) {
 #pragma unroll
   for (int i = 0; i < P::N; i++) a.v[i] = ge ? t.v[i] : a.v[i];
 }
+// Limb i of 2p in "borrowed" form: each limb below the top takes 2^29 - 1 from
+// its upper neighbour (limb 0: 2^29), so c_i >= s_i for every normalised s < 2p
+// and c - s needs no carries.  Same integer as 2p.
+template <class P>
+GM_HD constexpr uint32_t p2_borrowed_limb(int i) {
+  return i == 0 ? kp_limb<P, 2>(0) + (1u << RADIX)
+                : (i == P::N - 1 ? kp_limb<P, 2>(i) - 1u : kp_limb<P, 2>(i) + (1u << RADIX) - 1u);
+}
+// neg ? 2p - s : s for s < 2p with normalised limbs, carry-free (2 VOP2 per limb
+// instead of a borrow chain plus a masked add of p).  The limbs of 2p - s are left
+// unnormalised (< 2^30; the top limb may read -1 as int32): the result may only
+// feed fe_sub_lz / fe_sub2x_lz as their minuend, whose signed carry pass
+// normalises it.  Value in (0, 2p].
+template <class P>
+GM_DEV Fe<P> fe_cneg2p_cf(const Fe<P>& s, bool neg) {
+  Fe<P> r;
+#pragma unroll
+  for (int i = 0; i < P::N; i++) r.v[i] = neg ? p2_borrowed_limb<P>(i) - s.v[i] : s.v[i];
+  return r;
+}
+// a - b - 2c + K p in one signed carry pass (b + 2c < K p; b, c normalised, a as
+// fe_sub_lz accepts it).  Replaces sub_lz(sub_lz(a, b), add_lz(c, c)): one
+// borrow chain instead of three.  The result is < a + K p.
+template <int K, class P>
+GM_DEV Fe<P> fe_sub2x_lz(const Fe<P>& a, const Fe<P>& b, const Fe<P>& c) {
+  Fe<P> r;
+  int32_t cy = 0;
+#pragma unroll
+  for (int i = 0; i < P::N; i++) {
+    const int32_t d = (int32_t)(a.v[i] + kp_limb<P, K>(i)) - (int32_t)(b.v[i] + (c.v[i] << 1)) + cy;
+    cy = d >> RADIX;
+    r.v[i] = i == P::N - 1 ? (uint32_t)d : ((uint32_t)d & LIMB_MASK);
+  }
+  return r;
+}
 // canonical representative of a < 2^L p (L <= 4)
 template <int L, class P>
 GM_DEV Fe<P> fe_canon(Fe<P> a) {

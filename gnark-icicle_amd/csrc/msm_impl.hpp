@@ -438,19 +438,25 @@ GM_DEV PackedPt<PW> load_packed_pt(const uint32_t* __restrict__ src) {
 template <class F>
 struct LazyAcc {
   static constexpr bool on = false;
-  GM_DEV static void add(XYZZ<F>& a, const Affine<F>& p) { xyzz_add_aff(a, p); }
+  GM_DEV static void add(XYZZ<F>& a, Affine<F> p, bool neg) {
+    if (neg) p.y = fe_neg(p.y);
+    xyzz_add_aff(a, p);
+  }
   GM_DEV static XYZZ<F> canon(const XYZZ<F>& a) { return a; }
 };
 template <class P>
 struct LazyAcc<Fe<P>> {
   static constexpr bool on = true;
-  GM_DEV static void add(XYZZ<Fe<P>>& a, const Affine<Fe<P>>& p) { xyzz_add_aff_lz(a, p); }
+  GM_DEV static void add(XYZZ<Fe<P>>& a, const Affine<Fe<P>>& p, bool neg) { xyzz_add_aff_lz(a, p, neg); }
   GM_DEV static XYZZ<Fe<P>> canon(const XYZZ<Fe<P>>& a) { return xyzz_canon_lz(a); }
 };
 template <class P, int B>
 struct LazyAcc<Fe2<P, B>> {
   static constexpr bool on = true;
-  GM_DEV static void add(XYZZ<Fe2<P, B>>& a, const Affine<Fe2<P, B>>& p) { xyzz_add_aff_lz(a, p); }
+  GM_DEV static void add(XYZZ<Fe2<P, B>>& a, Affine<Fe2<P, B>> p, bool neg) {
+    if (neg) p.y = fe_neg(p.y);
+    xyzz_add_aff_lz(a, p);
+  }
   GM_DEV static XYZZ<Fe2<P, B>> canon(const XYZZ<Fe2<P, B>>& a) { return xyzz_canon_lz(a); }
 };
 
@@ -516,8 +522,7 @@ GM_DEV void accum_seg_body(const uint32_t* __restrict__ points, uint32_t n,
     }
     if (!PREFETCH) P = load_packed_pt<PW>(points + (size_t)(v & 0x7fffffffu) * PW);
     Affine<F> A = load_affine_packed<F>(P.w);
-    if (v >> 31) A.y = fe_neg(A.y);
-    LazyAcc<F>::add(acc, A);
+    LazyAcc<F>::add(acc, A, (v >> 31) != 0);
     if (PREFETCH) {
       v = vn;
       P = Pn;
@@ -533,15 +538,40 @@ GM_DEV void accum_seg_body(const uint32_t* __restrict__ points, uint32_t n,
 }
 
 
-// G1: the next point is prefetched into registers while the current add runs.
+// G1 default: four waves per SIMD (<= 128 VGPRs, no spill) and no prefetch --
+// the other waves hide the point loads and the mad-chain latency.  Same-box A/B
+// at 2^20 (profiles/r03e_ab.txt): 1.335 ms vs 1.343-1.358 ms for the 3-wave
+// prefetching kernel (k_msm_accum_seg_pf, GM_MSM_ACCUM=prefetch), 1.53 ms with
+// prefetch at four waves (36 VGPRs spilled); precomputed keys 1.41-1.46 vs 1.47.
 template <class F>
-__global__ void __launch_bounds__(128) k_msm_accum_seg(const uint32_t* __restrict__ points, uint32_t n,
-                                                       const uint32_t* __restrict__ keys,
-                                                       const uint32_t* __restrict__ vals,
-                                                       const uint32_t* __restrict__ offsets, uint32_t total,
-                                                       uint32_t K, XYZZ<F>* __restrict__ buckets,
-                                                       XYZZ<F>* __restrict__ part_first,
-                                                       XYZZ<F>* __restrict__ part_last, uint32_t* __restrict__ err) {
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4)))
+k_msm_accum_seg(const uint32_t* __restrict__ points, uint32_t n, const uint32_t* __restrict__ keys,
+                const uint32_t* __restrict__ vals, const uint32_t* __restrict__ offsets, uint32_t total,
+                uint32_t K, XYZZ<F>* __restrict__ buckets, XYZZ<F>* __restrict__ part_first,
+                XYZZ<F>* __restrict__ part_last, uint32_t* __restrict__ err) {
+  accum_seg_body<F, false>(points, n, keys, vals, offsets, total, K, buckets, part_first, part_last, err);
+}
+// Four waves fit the 9-limb fields only: BLS12-377's 14-limb add spills 216
+// VGPRs under the cap and keeps the prefetching kernel (2 waves, no spill).
+template <class F>
+struct AccumW4 {
+  static constexpr bool ok = false;
+};
+template <class P>
+struct AccumW4<Fe<P>> {
+  static constexpr bool ok = P::N <= 9;
+};
+// The next point prefetched into registers while the current add runs (three
+// waves per SIMD for BN254 G1, two for BLS12-377 G1).
+template <class F>
+__global__ void __launch_bounds__(128) k_msm_accum_seg_pf(const uint32_t* __restrict__ points, uint32_t n,
+                                                          const uint32_t* __restrict__ keys,
+                                                          const uint32_t* __restrict__ vals,
+                                                          const uint32_t* __restrict__ offsets, uint32_t total,
+                                                          uint32_t K, XYZZ<F>* __restrict__ buckets,
+                                                          XYZZ<F>* __restrict__ part_first,
+                                                          XYZZ<F>* __restrict__ part_last,
+                                                          uint32_t* __restrict__ err) {
   accum_seg_body<F, true>(points, n, keys, vals, offsets, total, K, buckets, part_first, part_last, err);
 }
 
@@ -1044,12 +1074,11 @@ int msm_launch(gm_ctx* ctx, Arena& arena, const MsmPlan& plan, const void* point
     GM_HIP(hipMemsetAsync(buckets.p, 0, sizeof(XYZZ<DF>) * (size_t)t.total, st));  // all-zero XYZZ = infinity
     ProfScope ps(ctx, G2 ? "msm_accum_g2" : "msm_accum_g1");
     // G2 defaults to lane pairs; GM_MSM_ACCUM=prefetch|noprefetch selects the
-    // one-lane kernels instead (tuning / A-B)
+    // one-lane kernels instead (tuning / A-B); for G1, prefetch selects the
+    // three-wave prefetching kernel
     static const char* ov = getenv("GM_MSM_ACCUM");
     bool pair = G2 && g2_pairs();
-    bool noprefetch = G2;
-    if (ov && !strcmp(ov, "prefetch")) noprefetch = false;
-    if (ov && !strcmp(ov, "noprefetch")) noprefetch = true;
+    const bool prefetch = ov && !strcmp(ov, "prefetch");
     if constexpr (PairSel<DF>::ok) {
       if (pair) {
         hipLaunchKernelGGL(PairSel<DF>::kernel(), dim3(blocks_for(2 * nslices, 128)), dim3(128), 0, st,
@@ -1061,7 +1090,10 @@ int msm_launch(gm_ctx* ctx, Arena& arena, const MsmPlan& plan, const void* point
       pair = false;
     }
     if (!pair) {
-      auto accum = noprefetch ? k_msm_accum_seg_g2<DF> : k_msm_accum_seg<DF>;
+      auto accum = prefetch ? k_msm_accum_seg_pf<DF> : (G2 ? k_msm_accum_seg_g2<DF> : k_msm_accum_seg_pf<DF>);
+      if constexpr (AccumW4<DF>::ok) {
+        if (!prefetch) accum = k_msm_accum_seg<DF>;
+      }
       hipLaunchKernelGGL(accum, dim3(blocks_for(nslices, 128)), dim3(128), 0, st,
                          reinterpret_cast<const uint32_t*>(points_internal), (uint32_t)plan.npts, plan.keys,
                          plan.vals, plan.offsets, t.total, t.K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(),

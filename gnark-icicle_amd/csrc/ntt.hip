@@ -48,9 +48,10 @@ GM_DEV uint32_t brev_bits(uint32_t x, int bits) { return bits ? (__brev(x) >> (3
 //   pre     first pass only: multiply on load (coset powers)
 //   post    last pass only: multiply on store (1/n, coset^-1, 1/(g^n - 1))
 //
-// Butterflies are Harvey-style lazy: tile values live in [0, 2p) between stages
-// (no final subtraction in the twiddle product, 2p offsets instead of sign
-// tests; field.hpp "Lazily reduced arithmetic"), canonical again on store.
+// Butterflies are Harvey-style lazy: tile values live in [0, 2p) (DIF) or
+// [0, 4p) (DIT) between stages (no final subtraction in the twiddle product, 2p
+// offsets instead of sign tests; field.hpp "Lazily reduced arithmetic"): one
+// conditional subtraction per butterfly, canonical again on store.
 //
 // Butterfly enumeration of a stage with half-size m = 2^lm (NBF = 512 per tile):
 //  * m <= 2: twiddle-index-major, so each wave shares one twiddle index jj and the
@@ -115,8 +116,13 @@ __global__ void __launch_bounds__(NTT_TPB) k_ntt_pass(Fe<P>* __restrict__ data, 
   }
   __syncthreads();
 
+  // Stages with lm >= 2 mix twiddle indices inside a wave (jj = 0 next to jj != 0
+  // lanes), so a jj == 0 branch would cost those waves the multiplication AND the
+  // reduction: there every lane multiplies (SW[0] = 1).  Stages lm <= 1 are
+  // twiddle-index-major, i.e. wave-uniform, and keep the skip.
   constexpr int NBF = NTT_TILE / 2;  // butterflies per stage
   if (!DIT) {
+    // inputs < 2p: s < 4p -> one conditional subtraction; d = (u - v + 2p) w < 2p
     for (int lm = t - 1; lm >= 0; lm--) {
       const int m = 1 << lm, step = T >> (lm + 1);
       for (int q = threadIdx.x; q < NBF; q += NTT_TPB) {
@@ -128,8 +134,10 @@ __global__ void __launch_bounds__(NTT_TPB) k_ntt_pass(Fe<P>* __restrict__ data, 
         fe_reduce_k<2>(s);
         X[j0 * B + ol] = s;
         Fe<P> d = fe_sub_lz<2>(u, v);                 // < 4p
-        if (jj) {
+        if (lm >= 2) {                                // block-uniform branch
           d = fe_mul_lz(d, SW[jj * step]);            // 4p * p < R' p: < 2p
+        } else if (jj) {
+          d = fe_mul_lz(d, SW[jj * step]);
         } else {
           fe_reduce_k<2>(d);
         }
@@ -138,20 +146,26 @@ __global__ void __launch_bounds__(NTT_TPB) k_ntt_pass(Fe<P>* __restrict__ data, 
       __syncthreads();
     }
   } else {
+    // Harvey: tile values < 4p; u -> < 2p (one conditional subtraction),
+    // v w < 2p, then s = u + v w and d = u - v w + 2p are both < 4p unreduced.
     for (int lm = 0; lm < t; lm++) {
       const int m = 1 << lm, step = T >> (lm + 1);
       for (int q = threadIdx.x; q < NBF; q += NTT_TPB) {
         int jj, ol, grp;
         bfly_index(q, lm, lgB, jj, ol, grp);
         const int j0 = (grp << (lm + 1)) + jj, j1 = j0 + m;
-        const Fe<P> u = X[j0 * B + ol];
+        Fe<P> u = X[j0 * B + ol];
         Fe<P> v = X[j1 * B + ol];
-        if (jj) v = fe_mul_lz(v, SW[jj * step]);      // < 2p
-        Fe<P> s = fe_add_lz(u, v), d = fe_sub_lz<2>(u, v);  // both < 4p
-        fe_reduce_k<2>(s);
-        fe_reduce_k<2>(d);
-        X[j0 * B + ol] = s;
-        X[j1 * B + ol] = d;
+        fe_reduce_k<2>(u);                            // < 2p
+        if (lm >= 2) {                                // block-uniform branch
+          v = fe_mul_lz(v, SW[jj * step]);            // 4p * p < R' p: < 2p
+        } else if (jj) {
+          v = fe_mul_lz(v, SW[jj * step]);
+        } else {
+          fe_reduce_k<2>(v);
+        }
+        X[j0 * B + ol] = fe_add_lz(u, v);             // < 4p
+        X[j1 * B + ol] = fe_sub_lz<2>(u, v);          // < 4p
       }
       __syncthreads();
     }
@@ -170,10 +184,13 @@ __global__ void __launch_bounds__(NTT_TPB) k_ntt_pass(Fe<P>* __restrict__ data, 
     if (o >= nother) continue;
     const size_t hi = o >> lo, L = o & lomask;
     const size_t addr = (hi << (lo + t)) + ((size_t)j << lo) + L;
-    Fe<P> v = X[j * B + ol];  // < 2p (lazy butterflies); canonical before the store
+    Fe<P> v = X[j * B + ol];  // < 2p (DIF) / < 4p (DIT); canonical before the store
     if (!DIT && lo > 0) v = fe_mul(v, ld_tab(tw, ((size_t)j << lo) + L));
     if (post) v = fe_mul(v, ld_tab(post, addr));
-    if (!(!DIT && lo > 0) && !post) fe_reduce_once(v);
+    if (!(!DIT && lo > 0) && !post) {
+      if (DIT) fe_reduce_k<2>(v);
+      fe_reduce_once(v);
+    }
     st_fe(data, addr, v);
   }
 }

@@ -122,23 +122,39 @@ GM_DEV PXYZZ<P> pxyzz_dbl_aff(const Fe<P>& px, const Fe<P>& py) {
   return r;
 }
 
-// a += P (P affine, canonical components; infinity (0,0) skipped).  Invariants
-// on a: every component < 2p (as xyzz_add_aff_lz for Fe2).
+// a += (neg ? -P : P) (P affine, canonical components; infinity (0,0)
+// skipped).  Invariants on a: every component < 2p (as xyzz_add_aff_lz for
+// Fe2).  BN254: as in the G1 add, the sign goes onto S2 (carry-free 2p - S2 per
+// component) and X3 takes one borrow chain (G2 2^20 accumulation 5.18 -> 5.13
+// ms).  BLS12-377 keeps y negated up front and three chains: its 14-limb add
+// already spills at three waves per SIMD, and the trimmed form spilled more
+// (171 -> 185 VGPRs, 2^22 accumulation 46.5 -> 47.4 ms; profiles/r03e_ab.txt).
 template <class P, int BETA>
-GM_DEV void pxyzz_add_aff(PXYZZ<P>& a, const Fe<P>& px, const Fe<P>& py) {
+GM_DEV void pxyzz_add_aff(PXYZZ<P>& a, const Fe<P>& px, const Fe<P>& py_in, bool neg) {
   static_assert(P::BITS + 7 <= RADIX * P::N, "lazy reduction needs R' > 128 p");
-  if (pair_all(fe_is_zero(px) && fe_is_zero(py))) return;
+  constexpr bool TRIM = P::N <= 9;
+  if (pair_all(fe_is_zero(px) && fe_is_zero(py_in))) return;
+  Fe<P> py = py_in;
+  if constexpr (!TRIM) {
+    if (neg) py = fe_neg(py_in);
+  }
   if (pxyzz_is_inf(a)) {
     a.x = px;
-    a.y = py;
+    a.y = (TRIM && neg) ? fe_neg(py) : py;
     a.zz = pair_odd() ? fe_zero<P>() : fe_one<P>();
     a.zzz = a.zz;
     return;
   }
   const Fe<P> Pd = fe_sub_lz<2>(pf2_mul<P, BETA>(px, a.zz), a.x);    // U2 - X1   < 4p
-  const Fe<P> R = fe_sub_lz<2>(pf2_mul<P, BETA>(py, a.zzz), a.y);    // S2 - Y1   < 4p
+  Fe<P> R;                                                          // +-S2 - Y1 < 4p
+  if constexpr (TRIM) {
+    // S2 < 2p; 2p - S2 in (0, 2p]
+    R = fe_sub_lz<2>(fe_cneg2p_cf(pf2_mul<P, BETA>(py, a.zzz), neg), a.y);
+  } else {
+    R = fe_sub_lz<2>(pf2_mul<P, BETA>(py, a.zzz), a.y);
+  }
   if (pair_all(fe_is_zero_lz<4>(Pd))) {
-    if (pair_all(fe_is_zero_lz<4>(R))) a = pxyzz_dbl_aff<P, BETA>(px, py);
+    if (pair_all(fe_is_zero_lz<4>(R))) a = pxyzz_dbl_aff<P, BETA>(px, (TRIM && neg) ? fe_neg(py) : py);
     else a = pxyzz_inf<P>();
     return;
   }
@@ -147,7 +163,12 @@ GM_DEV void pxyzz_add_aff(PXYZZ<P>& a, const Fe<P>& px, const Fe<P>& py) {
   a.zz = pf2_mul<P, BETA>(a.zz, PP);
   const Fe<P> Q = pf2_mul<P, BETA>(a.x, PP);                        // < 2p
   a.zzz = pf2_mul<P, BETA>(a.zzz, PPP);
-  Fe<P> X3 = fe_sub_lz<4>(fe_sub_lz<2>(pf2_sqr<P, BETA, 4>(R), PPP), fe_add_lz(Q, Q));  // < 8p
+  Fe<P> X3;                                                         // < 8p
+  if constexpr (TRIM) {
+    X3 = fe_sub2x_lz<6>(pf2_sqr<P, BETA, 4>(R), PPP, Q);
+  } else {
+    X3 = fe_sub_lz<4>(fe_sub_lz<2>(pf2_sqr<P, BETA, 4>(R), PPP), fe_add_lz(Q, Q));
+  }
   fe_to2p<8>(X3);
   Fe<P> Y3 = fe_sub_lz<2>(pf2_mul<P, BETA>(R, fe_sub_lz<2>(Q, X3)), pf2_mul<P, BETA>(a.y, PPP));  // < 4p
   fe_to2p<4>(Y3);
@@ -246,9 +267,8 @@ __global__ void __launch_bounds__(128) GM_PAIR_ATTR k_msm_accum_seg_pair(const u
       cur = k;
     }
     const Fe<P> px = fe_unpack<P>(pt.x);
-    Fe<P> py = fe_unpack<P>(pt.y);
-    if (v >> 31) py = fe_neg(py);
-    pxyzz_add_aff<P, BETA>(acc, px, py);
+    const Fe<P> py = fe_unpack<P>(pt.y);
+    pxyzz_add_aff<P, BETA>(acc, px, py, (v >> 31) != 0);
     v = vn;
     pt = ptn;
   }
