@@ -27,8 +27,11 @@ sys.path.insert(0, os.path.join(ROOT, "gnark-icicle_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (8.0 TB/s spec)
 MSM_BYTES_PER_POINT = 96  # 64 B affine point + 32 B scalar
-# radix-2^29 BN254 Fp (9 limbs): mul = 2*81 mads, sqr = 45 + 81; mixed add = 8M + 2S
-MADS_PER_MIXED_ADD = 8 * 162 + 2 * 126
+# radix-2^29 BN254 Fp (9 limbs): mul = 2*81 mads, sqr = 45 + 81; the mixed add is
+# 8M + 2S with Y3 = R (Q - X3) - Y1 PPP as one reduction of two products (243):
+# 6*162 + 2*126 + 243 = 1467 v_mad_u64_u32, the count in the kernel's ISA
+# (tools/isa_blocks.py on the hipcc -S listing)
+MADS_PER_MIXED_ADD = 6 * 162 + 2 * 126 + 243
 # measured v_mad_u64_u32 issue peak: 5.12 cycles per wave64 instruction per SIMD with
 # 8 independent chains at 8 waves/SIMD (tools/microbench/isa_rate.hip,
 # profiles/r01_isa_rate.txt): 1024 SIMDs x 64 lanes x 2.4 GHz / 5.12 = 30.7 T/s
@@ -56,7 +59,7 @@ def parse():
 
 def load_pmc_traffic(name):
     """HBM bytes per launch from a committed rocprofv3 --pmc summary (or None)."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    p = os.path.join(ROOT, "profiles", "r03h_pmc_traffic.json")
     try:
         with open(p) as f:
             return json.load(f).get(name)
@@ -66,7 +69,7 @@ def load_pmc_traffic(name):
 
 def load_pmc_valu(name):
     """VALU utilisation of a kernel from the committed PMC summary (or None)."""
-    p = os.path.join(ROOT, "profiles", "r02_pmc_valu.json")
+    p = os.path.join(ROOT, "profiles", "r03h_pmc_valu.json")
     try:
         with open(p) as f:
             return json.load(f).get(name)
@@ -178,8 +181,8 @@ def main():
                         npts, "GLV (P, phi(P)) " if glv else "", windows, MADS_PER_MIXED_ADD)},
         "valu": load_pmc_valu("k_msm_accum_seg<Fe<Bn254Fp> >"),
         "note": "bound=hbm is the bench contract's roofline for this non-MFMA path; the kernel is NOT HBM-bound: "
-                "its binding resource is VALU issue -- rocprofv3 PMC (profiles/r02_pmc_valu.json) shows VALUBusy "
-                "~0.89 (gfx9 formula, 4 cycles/instr) for k_msm_accum_seg, ~2750 VALU instructions per mixed add; "
+                "its binding resource is VALU issue -- rocprofv3 PMC (profiles/r03h_pmc_valu.json) shows VALUBusy "
+                "~0.87 (gfx9 formula, 4 cycles/instr) for k_msm_accum_seg, ~2560 VALU instructions per mixed add; "
                 "int_alu prices the v_mad_u64_u32 work at the measured mad-only issue peak (DESIGN.md section 3)",
     }
     kernel_ms = {k: round(v[0] / max(v[1], 1), 4) for k, v in stats.items()}

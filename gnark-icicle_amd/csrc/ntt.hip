@@ -13,6 +13,8 @@
 // low bits with the twiddle after the sub-transform; DIT is the transpose:
 // low -> high with the twiddle before.  Three passes cover 2^24 (8+8+8), i.e.
 // three HBM round trips instead of 24.
+#include <cstdlib>
+
 #include "curves.hpp"
 #include "ntt.hpp"
 #include "runtime.hpp"
@@ -74,8 +76,11 @@ GM_DEV void bfly_index(int q, int lm, int lgB, int& jj, int& ol, int& grp) {
   }
 }
 
-template <class P, bool DIT>
-__global__ void __launch_bounds__(NTT_TPB) k_ntt_pass(Fe<P>* __restrict__ data, int logn, int lo,
+// TPB threads per tile (256, or 512: one butterfly per thread and stage);
+// SWG: sub-transform twiddles read through the cache instead of staged in LDS
+// (36 KiB instead of 41.5 KiB of LDS per block: four blocks per CU).
+template <class P, bool DIT, int TPB = NTT_TPB, bool SWG = false>
+__global__ void __launch_bounds__(TPB) k_ntt_pass(Fe<P>* __restrict__ data, int logn, int lo,
                                                       int t, const Fe<P>* __restrict__ tw,
                                                       const Fe<P>* __restrict__ sub,
                                                       const Fe<P>* __restrict__ pre,
@@ -84,7 +89,7 @@ __global__ void __launch_bounds__(NTT_TPB) k_ntt_pass(Fe<P>* __restrict__ data, 
                                                       const Fe<P>* __restrict__ pc) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   Fe<P>* X = reinterpret_cast<Fe<P>*>(smem_raw);   // [T][B]
-  Fe<P>* SW = X + NTT_TILE;                         // [T/2]
+  Fe<P>* SWl = X + NTT_TILE;                        // [T/2]
   const int T = 1 << t;
   const int lgB = NTT_TILE_LOG - t;
   const int B = 1 << lgB;
@@ -92,10 +97,12 @@ __global__ void __launch_bounds__(NTT_TPB) k_ntt_pass(Fe<P>* __restrict__ data, 
   const size_t o0 = (size_t)blockIdx.x * B;
   const size_t lomask = ((size_t)1 << lo) - 1;
 
-  for (int x = threadIdx.x; x < T / 2; x += NTT_TPB) SW[x] = ld_tab(sub, x);
+  if (!SWG)
+    for (int x = threadIdx.x; x < T / 2; x += TPB) SWl[x] = ld_tab(sub, x);
+  const Fe<P>* __restrict__ SW = SWG ? sub : SWl;
 
   // load (j, o) -> X[j*B + o]
-  for (int q = threadIdx.x; q < NTT_TILE; q += NTT_TPB) {
+  for (int q = threadIdx.x; q < NTT_TILE; q += TPB) {
     int j, ol;
     if (lo == 0) {
       j = q & (T - 1);
@@ -125,7 +132,7 @@ __global__ void __launch_bounds__(NTT_TPB) k_ntt_pass(Fe<P>* __restrict__ data, 
     // inputs < 2p: s < 4p -> one conditional subtraction; d = (u - v + 2p) w < 2p
     for (int lm = t - 1; lm >= 0; lm--) {
       const int m = 1 << lm, step = T >> (lm + 1);
-      for (int q = threadIdx.x; q < NBF; q += NTT_TPB) {
+      for (int q = threadIdx.x; q < NBF; q += TPB) {
         int jj, ol, grp;
         bfly_index(q, lm, lgB, jj, ol, grp);
         const int j0 = (grp << (lm + 1)) + jj, j1 = j0 + m;
@@ -150,7 +157,7 @@ __global__ void __launch_bounds__(NTT_TPB) k_ntt_pass(Fe<P>* __restrict__ data, 
     // v w < 2p, then s = u + v w and d = u - v w + 2p are both < 4p unreduced.
     for (int lm = 0; lm < t; lm++) {
       const int m = 1 << lm, step = T >> (lm + 1);
-      for (int q = threadIdx.x; q < NBF; q += NTT_TPB) {
+      for (int q = threadIdx.x; q < NBF; q += TPB) {
         int jj, ol, grp;
         bfly_index(q, lm, lgB, jj, ol, grp);
         const int j0 = (grp << (lm + 1)) + jj, j1 = j0 + m;
@@ -171,7 +178,7 @@ __global__ void __launch_bounds__(NTT_TPB) k_ntt_pass(Fe<P>* __restrict__ data, 
     }
   }
 
-  for (int q = threadIdx.x; q < NTT_TILE; q += NTT_TPB) {
+  for (int q = threadIdx.x; q < NTT_TILE; q += TPB) {
     int j, ol;
     if (lo == 0) {
       j = q & (T - 1);
@@ -504,7 +511,11 @@ static int run_passes(gm_ctx* ctx, NttDomain<C>* d, Fe<typename C::Fr>* a, bool 
                       const NttFuse<typename C::Fr>& fz) {
   using Fr = typename C::Fr;
   hipStream_t st = ctx->stream;
-  const size_t smem = sizeof(Fe<Fr>) * (NTT_TILE + (1 << (NTT_TMAX - 1)));
+  // GM_NTT_TPB=512: one butterfly per thread and stage; GM_NTT_SWG=1: twiddles
+  // through the cache (LDS holds the tile only)
+  static const int tpb = getenv("GM_NTT_TPB") ? atoi(getenv("GM_NTT_TPB")) : NTT_TPB;
+  static const bool swg = getenv("GM_NTT_SWG") && atoi(getenv("GM_NTT_SWG")) != 0;
+  const size_t smem = sizeof(Fe<Fr>) * (NTT_TILE + (swg ? 0 : (1 << (NTT_TMAX - 1))));
   const int np = (int)d->passes.size();
   for (int k = 0; k < np; k++) {
     const int pi = dit ? np - 1 - k : k;
@@ -518,7 +529,10 @@ static int run_passes(gm_ctx* ctx, NttDomain<C>* d, Fe<typename C::Fr>* a, bool 
     const unsigned grid = (unsigned)((nother + B - 1) / B);
     ProfScope pscope(ctx, "ntt_pass");
     auto kern = dit ? k_ntt_pass<Fr, true> : k_ntt_pass<Fr, false>;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(NTT_TPB), smem, st, a, d->logn, ps.lo, ps.t, tw, sub,
+    if (tpb == 512) kern = dit ? (swg ? k_ntt_pass<Fr, true, 512, true> : k_ntt_pass<Fr, true, 512>)
+                               : (swg ? k_ntt_pass<Fr, false, 512, true> : k_ntt_pass<Fr, false, 512>);
+    else if (swg) kern = dit ? k_ntt_pass<Fr, true, NTT_TPB, true> : k_ntt_pass<Fr, false, NTT_TPB, true>;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(tpb == 512 ? 512 : NTT_TPB), smem, st, a, d->logn, ps.lo, ps.t, tw, sub,
                        first ? fz.pre : nullptr, last ? fz.post : nullptr, first ? fz.pb : nullptr,
                        first ? fz.pc : nullptr);
   }
