@@ -595,7 +595,20 @@ struct PairSel {
 template <class P, int B>
 struct PairSel<Fe2<P, B>> {
   static constexpr bool ok = true;
-  static constexpr auto kernel() { return k_msm_accum_seg_pair<P, B>; }
+  // Point prefetch: on for BN254; off for BLS12-377, whose pair kernel spills
+  // at three waves per SIMD (171 -> 135 VGPRs without the prefetch registers;
+  // 2^22 accumulation 46.1 -> 44.2 ms, profiles/r03i_ab.txt).  GM_MSM_PAIR_PF=0/1
+  // overrides.
+  // GM_MSM_PAIR_WPE=3 (A/B): BN254 without prefetch capped at three waves.
+  static auto kernel() {
+    static const char* pf = getenv("GM_MSM_PAIR_PF");
+    static const char* wpe = getenv("GM_MSM_PAIR_WPE");
+    const bool on = pf ? pf[0] != '0' : P::N <= 9;
+    if constexpr (P::N <= 9) {
+      if (wpe && wpe[0] == '3') return k_msm_accum_seg_pair<P, B, false, 3>;
+    }
+    return on ? k_msm_accum_seg_pair<P, B, true> : k_msm_accum_seg_pair<P, B, false>;
+  }
   static constexpr auto fixup() { return k_msm_fixup_pair<P, B>; }
   static constexpr auto fix_tree() { return k_msm_fix_tree_pair<P, B>; }
   static constexpr auto fixup_long() { return k_msm_fixup_long_pair<P, B>; }

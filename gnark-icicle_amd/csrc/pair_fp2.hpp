@@ -213,9 +213,12 @@ GM_DEV PairPt<P> pair_load_pt(const uint32_t* __restrict__ pt) {
 #ifndef GM_PAIR_WPE
 #define GM_PAIR_WPE 1  // no cap; per-TU override (msm_bls12377_g2.hip)
 #endif
-#define GM_PAIR_ATTR __attribute__((amdgpu_waves_per_eu(GM_PAIR_WPE)))
-template <class P, int BETA>
-__global__ void __launch_bounds__(128) GM_PAIR_ATTR k_msm_accum_seg_pair(const uint32_t* __restrict__ points, uint32_t n,
+// PF: prefetch the next point's components (2 x NG registers) while the
+// current add runs; without it the other waves hide the load (GM_MSM_PAIR_PF=0).
+// WPE: waves-per-SIMD floor for the register allocator (1 = no cap).
+template <class P, int BETA, bool PF = true, int WPE = GM_PAIR_WPE>
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE)))
+k_msm_accum_seg_pair(const uint32_t* __restrict__ points, uint32_t n,
                                                             const uint32_t* __restrict__ keys,
                                                             const uint32_t* __restrict__ vals,
                                                             const uint32_t* __restrict__ offsets, uint32_t total,
@@ -258,8 +261,9 @@ __global__ void __launch_bounds__(128) GM_PAIR_ATTR k_msm_accum_seg_pair(const u
         if (!pair_odd()) atomicOr(err, 2u);
         return;
       }
-      ptn = pair_load_pt<P>(points + (size_t)(vn & 0x7fffffffu) * 4 * P::NG);
+      if (PF) ptn = pair_load_pt<P>(points + (size_t)(vn & 0x7fffffffu) * 4 * P::NG);
     }
+    if (!PF) pt = pair_load_pt<P>(points + (size_t)(v & 0x7fffffffu) * 4 * P::NG);
     if (k != cur) {
       emit(cur, acc, first, false);
       first = false;
@@ -270,7 +274,7 @@ __global__ void __launch_bounds__(128) GM_PAIR_ATTR k_msm_accum_seg_pair(const u
     const Fe<P> py = fe_unpack<P>(pt.y);
     pxyzz_add_aff<P, BETA>(acc, px, py, (v >> 31) != 0);
     v = vn;
-    pt = ptn;
+    if (PF) pt = ptn;
   }
   emit(cur, acc, first, true);
 }
