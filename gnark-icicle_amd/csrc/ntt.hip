@@ -132,6 +132,34 @@ __global__ void __launch_bounds__(TPB) k_ntt_pass(Fe<P>* __restrict__ data, int 
     // inputs < 2p: s < 4p -> one conditional subtraction; d = (u - v + 2p) w < 2p
     for (int lm = t - 1; lm >= 0; lm--) {
       const int m = 1 << lm, step = T >> (lm + 1);
+      if (lm >= 2 && NBF == 2 * TPB) {
+        // two butterflies per thread, loads first: two independent product chains
+        int jj[2], ol[2], grp[2], i0[2], i1[2];
+        Fe<P> u[2], v[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          bfly_index(threadIdx.x + h * TPB, lm, lgB, jj[h], ol[h], grp[h]);
+          const int j0 = (grp[h] << (lm + 1)) + jj[h];
+          i0[h] = j0 * B + ol[h];
+          i1[h] = (j0 + m) * B + ol[h];
+          u[h] = X[i0[h]];
+          v[h] = X[i1[h]];
+        }
+        Fe<P> s[2], d[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          s[h] = fe_add_lz(u[h], v[h]);               // < 4p
+          fe_reduce_k<2>(s[h]);
+          d[h] = fe_mul_lz(fe_sub_lz<2>(u[h], v[h]), SW[jj[h] * step]);  // < 2p
+        }
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          X[i0[h]] = s[h];
+          X[i1[h]] = d[h];
+        }
+        __syncthreads();
+        continue;
+      }
       for (int q = threadIdx.x; q < NBF; q += TPB) {
         int jj, ol, grp;
         bfly_index(q, lm, lgB, jj, ol, grp);
@@ -157,6 +185,32 @@ __global__ void __launch_bounds__(TPB) k_ntt_pass(Fe<P>* __restrict__ data, int 
     // v w < 2p, then s = u + v w and d = u - v w + 2p are both < 4p unreduced.
     for (int lm = 0; lm < t; lm++) {
       const int m = 1 << lm, step = T >> (lm + 1);
+      if (lm >= 2 && NBF == 2 * TPB) {
+        // two butterflies per thread, loads first: two independent product chains
+        int jj[2], ol[2], grp[2], i0[2], i1[2];
+        Fe<P> u[2], v[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          bfly_index(threadIdx.x + h * TPB, lm, lgB, jj[h], ol[h], grp[h]);
+          const int j0 = (grp[h] << (lm + 1)) + jj[h];
+          i0[h] = j0 * B + ol[h];
+          i1[h] = (j0 + m) * B + ol[h];
+          u[h] = X[i0[h]];
+          v[h] = X[i1[h]];
+        }
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          fe_reduce_k<2>(u[h]);                       // < 2p
+          v[h] = fe_mul_lz(v[h], SW[jj[h] * step]);   // < 2p
+        }
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          X[i0[h]] = fe_add_lz(u[h], v[h]);           // < 4p
+          X[i1[h]] = fe_sub_lz<2>(u[h], v[h]);        // < 4p
+        }
+        __syncthreads();
+        continue;
+      }
       for (int q = threadIdx.x; q < NBF; q += TPB) {
         int jj, ol, grp;
         bfly_index(q, lm, lgB, jj, ol, grp);
