@@ -565,10 +565,12 @@ static int run_passes(gm_ctx* ctx, NttDomain<C>* d, Fe<typename C::Fr>* a, bool 
                       const NttFuse<typename C::Fr>& fz) {
   using Fr = typename C::Fr;
   hipStream_t st = ctx->stream;
-  // GM_NTT_TPB=512: one butterfly per thread and stage; GM_NTT_SWG=1: twiddles
-  // through the cache (LDS holds the tile only)
+  // Twiddles are read through the cache by default (LDS holds the tile only:
+  // four blocks per CU; 1.5-2 % faster at 2^24 with the interleaved butterflies,
+  // profiles/r03m_ntt_swg_ab.txt); GM_NTT_SWG=0 stages them in LDS.
+  // GM_NTT_TPB=512: one butterfly per thread and stage (no gain measured).
   static const int tpb = getenv("GM_NTT_TPB") ? atoi(getenv("GM_NTT_TPB")) : NTT_TPB;
-  static const bool swg = getenv("GM_NTT_SWG") && atoi(getenv("GM_NTT_SWG")) != 0;
+  static const bool swg = getenv("GM_NTT_SWG") ? atoi(getenv("GM_NTT_SWG")) != 0 : true;
   const size_t smem = sizeof(Fe<Fr>) * (NTT_TILE + (swg ? 0 : (1 << (NTT_TMAX - 1))));
   const int np = (int)d->passes.size();
   for (int k = 0; k < np; k++) {
