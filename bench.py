@@ -114,22 +114,26 @@ def main():
             return gm.sharded_msm(ctx, "bn254", S, P, n)
         return ctx.msm("bn254", S, P, n)[0]
 
+    def finish(pend):
+        """Host tail of one step: this rank's partial, plus (N > 1) the all-gather
+        of every rank's 96-B partial and the host adds -- the full sharded MSM."""
+        local = pend.wait()[0]
+        if dist is None:
+            return local
+        return gm.reduce_partials("bn254", False, gm.allgather_partial(local))
+
     def run(k):
-        """k MSMs.  One GPU: pipelined two deep (gm_msm_async) -- step i+1's device
-        work is queued before step i's host tail (readback checks + Horner) runs,
-        so the host tail overlaps the GPU; every result is complete when run returns."""
-        if dist is not None:
-            r = None
-            for _ in range(k):
-                r = step()
-            return r
+        """k MSMs, pipelined two deep (gm_msm_async): step i+1's device work is
+        queued before step i's host tail (readback checks + Horner, and at N > 1
+        the RCCL all-gather of the partials and the host adds) runs, so the tail
+        overlaps the GPU; every result is complete when run returns."""
         pend, r = None, None
         for _ in range(k):
             nxt = ctx.msm_async("bn254", S, P, n)
             if pend is not None:
-                r = pend.wait()[0]
+                r = finish(pend)
             pend = nxt
-        return pend.wait()[0] if pend is not None else r
+        return finish(pend) if pend is not None else r
 
     run(args.warmup)
     # unpipelined latency of one MSM (synchronous gm_msm), for reference
@@ -204,8 +208,9 @@ def main():
                    "points_per_gpu": n, "total_points": total_points, "parallelism": "msm-shard%d" % world},
         "roofline": roofline,
         "kernel_avg_ms": kernel_ms,
-        "pipeline": "1 GPU: steps pipelined two deep (gm_msm_async / gm_msm_wait): step i+1's device work "
-                    "is queued before step i's host tail; latency_ms = one synchronous gm_msm",
+        "pipeline": "steps pipelined two deep (gm_msm_async / gm_msm_wait): step i+1's device work is queued "
+                    "before step i's host tail (N > 1: incl. the all-gather of partials and the host adds); "
+                    "latency_ms = one synchronous (N > 1: sharded) MSM",
         "latency_ms": round(lat_ms, 4),
     }
 
