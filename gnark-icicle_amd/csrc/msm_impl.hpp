@@ -475,7 +475,10 @@ GM_DEV void accum_emit(uint32_t b, const XYZZ<F>& acc_raw, bool is_first, bool i
   }
 }
 
-template <class F, bool PREFETCH>
+// PREFETCH: the next entry's point words are loaded while this add runs.
+// IDXPF (without PREFETCH): only the next entry's key and value are, so the
+// point address of each iteration is known when it starts.
+template <class F, bool PREFETCH, bool IDXPF = false>
 GM_DEV void accum_seg_body(const uint32_t* __restrict__ points, uint32_t n,
                                                        const uint32_t* __restrict__ keys,
                                                        const uint32_t* __restrict__ vals,
@@ -500,8 +503,14 @@ GM_DEV void accum_seg_body(const uint32_t* __restrict__ points, uint32_t n,
   }
   constexpr int PW = 2 * Coord<F>::WORDS;  // u32 words per packed point
   PackedPt<PW> P = load_packed_pt<PW>(points + (size_t)idx * PW);
+  uint32_t kq = keys[start];
   for (uint32_t q = start; q < end; q++) {
-    const uint32_t k = keys[q];
+    const uint32_t k = IDXPF ? kq : keys[q];
+    uint32_t vi = 0;
+    if (IDXPF && !PREFETCH && q + 1 < end) {
+      kq = keys[q + 1];
+      vi = vals[q + 1];
+    }
     // prefetch the next point's words while this add runs
     uint32_t vn = 0;
     PackedPt<PW> Pn;
@@ -527,7 +536,7 @@ GM_DEV void accum_seg_body(const uint32_t* __restrict__ points, uint32_t n,
       v = vn;
       P = Pn;
     } else if (q + 1 < end) {
-      v = vals[q + 1];
+      v = IDXPF ? vi : vals[q + 1];
       if ((v & 0x7fffffffu) >= n) {
         atomicOr(err, 2u);
         return;
@@ -550,6 +559,15 @@ k_msm_accum_seg(const uint32_t* __restrict__ points, uint32_t n, const uint32_t*
                 uint32_t K, XYZZ<F>* __restrict__ buckets, XYZZ<F>* __restrict__ part_first,
                 XYZZ<F>* __restrict__ part_last, uint32_t* __restrict__ err) {
   accum_seg_body<F, false>(points, n, keys, vals, offsets, total, K, buckets, part_first, part_last, err);
+}
+// Same with the next key / value prefetched (GM_MSM_ACCUM=idx; A-B).
+template <class F>
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4)))
+k_msm_accum_seg_idx(const uint32_t* __restrict__ points, uint32_t n, const uint32_t* __restrict__ keys,
+                    const uint32_t* __restrict__ vals, const uint32_t* __restrict__ offsets, uint32_t total,
+                    uint32_t K, XYZZ<F>* __restrict__ buckets, XYZZ<F>* __restrict__ part_first,
+                    XYZZ<F>* __restrict__ part_last, uint32_t* __restrict__ err) {
+  accum_seg_body<F, false, true>(points, n, keys, vals, offsets, total, K, buckets, part_first, part_last, err);
 }
 // Four waves fit the 9-limb fields only: BLS12-377's 14-limb add spills 216
 // VGPRs under the cap and keeps the prefetching kernel (2 waves, no spill).
@@ -1106,6 +1124,7 @@ int msm_launch(gm_ctx* ctx, Arena& arena, const MsmPlan& plan, const void* point
       auto accum = prefetch ? k_msm_accum_seg_pf<DF> : (G2 ? k_msm_accum_seg_g2<DF> : k_msm_accum_seg_pf<DF>);
       if constexpr (AccumW4<DF>::ok) {
         if (!prefetch) accum = k_msm_accum_seg<DF>;
+        if (ov && !strcmp(ov, "idx")) accum = k_msm_accum_seg_idx<DF>;
       }
       hipLaunchKernelGGL(accum, dim3(blocks_for(nslices, 128)), dim3(128), 0, st,
                          reinterpret_cast<const uint32_t*>(points_internal), (uint32_t)plan.npts, plan.keys,
