@@ -118,7 +118,8 @@ __global__ void __launch_bounds__(TPB) k_ntt_pass(Fe<P>* __restrict__ data, int 
     Fe<P> v = ld_fe(data, addr);
     if (pb) v = fe_sub(fe_mul(v, fe_to_internal(ld_fe(pb, addr))), ld_fe(pc, addr));
     if (pre) v = fe_mul(v, ld_tab(pre, addr));
-    if (DIT && lo > 0) v = fe_mul(v, ld_tab(tw, ((size_t)j << lo) + L));
+    // inter-pass twiddle, lazily reduced (< 2p; the DIT tile takes < 4p)
+    if (DIT && lo > 0) v = fe_mul_lz(v, ld_tab(tw, ((size_t)j << lo) + L));
     X[j * B + ol] = v;
   }
   __syncthreads();
@@ -246,7 +247,10 @@ __global__ void __launch_bounds__(TPB) k_ntt_pass(Fe<P>* __restrict__ data, int 
     const size_t hi = o >> lo, L = o & lomask;
     const size_t addr = (hi << (lo + t)) + ((size_t)j << lo) + L;
     Fe<P> v = X[j * B + ol];  // < 2p (DIF) / < 4p (DIT); canonical before the store
-    if (!DIT && lo > 0) v = fe_mul(v, ld_tab(tw, ((size_t)j << lo) + L));
+    // inter-pass twiddle of a DIF pass with lo > 0: never the last pass (that one
+    // has lo = 0), so the value is stored lazily reduced (< 2p) for the next
+    // pass, whose tile takes < 2p
+    if (!DIT && lo > 0) v = fe_mul_lz(v, ld_tab(tw, ((size_t)j << lo) + L));
     if (post) v = fe_mul(v, ld_tab(post, addr));
     if (!(!DIT && lo > 0) && !post) {
       if (DIT) fe_reduce_k<2>(v);
