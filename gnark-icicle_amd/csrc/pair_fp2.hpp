@@ -61,6 +61,49 @@ GM_DEV Fe<P> pf2_mul(const Fe<P>& a, const Fe<P>& b) {
   return r;
 }
 
+// x1 y1 + x2 y2 - x3 y3 - x4 y4 + p in ONE Montgomery reduction (signed columns:
+// the positive side of a column is <= 27 * 2^58 < 2^63 for N = 9, the negative
+// <= 18 * 2^58).  Inputs with normalised limbs; for the BN254 G2 Y3 below the
+// negative products are < 20 p^2 < p R', so the result is >= 0, and < 2.3p.
+template <class P>
+GM_DEV Fe<P> fe_mul4_redc(const Fe<P>& x1, const Fe<P>& y1, const Fe<P>& x2, const Fe<P>& y2, const Fe<P>& x3,
+                          const Fe<P>& y3, const Fe<P>& x4, const Fe<P>& y4) {
+  constexpr int N = P::N;
+  static_assert(N <= 9, "signed column bound needs N <= 9");
+  uint32_t m[N];
+  Fe<P> r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * N - 1; k++) {
+    uint64_t cp = 0, cn = 0;
+#pragma unroll
+    for (int i = (k - N + 1 > 0 ? k - N + 1 : 0); i <= (k < N - 1 ? k : N - 1); i++) {
+      cp += (uint64_t)x1.v[i] * y1.v[k - i] + (uint64_t)x2.v[i] * y2.v[k - i];
+      cn += (uint64_t)x3.v[i] * y3.v[k - i] + (uint64_t)x4.v[i] * y4.v[k - i];
+    }
+    acc += cp - cn;
+#pragma unroll
+    for (int i = (k - N + 1 > 0 ? k - N + 1 : 0); i <= (k - 1 < N - 1 ? k - 1 : N - 1); i++)
+      acc += (uint64_t)m[i] * P::p(k - i);
+    if (k < N) {
+      m[k] = ((uint32_t)acc * P::INV) & LIMB_MASK;
+      acc += (uint64_t)m[k] * P::p(0);
+    } else {
+      r.v[k - N] = (uint32_t)acc & LIMB_MASK;
+    }
+    acc = (uint64_t)((int64_t)acc >> RADIX);
+  }
+  r.v[N - 1] = (uint32_t)acc;  // two's complement top limb when negative
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < N; i++) {  // + p
+    const uint32_t sm = r.v[i] + P::p(i) + c;
+    r.v[i] = i == N - 1 ? sm : (sm & LIMB_MASK);
+    c = sm >> RADIX;
+  }
+  return r;
+}
+
 // Component of a^2, inputs < IN p per component, result < 2p.
 template <class P, int BETA, int IN>
 GM_DEV Fe<P> pf2_sqr(const Fe<P>& a) {
@@ -170,7 +213,18 @@ GM_DEV void pxyzz_add_aff(PXYZZ<P>& a, const Fe<P>& px, const Fe<P>& py_in, bool
     X3 = fe_sub_lz<4>(fe_sub_lz<2>(pf2_sqr<P, BETA, 4>(R), PPP), fe_add_lz(Q, Q));
   }
   fe_to2p<8>(X3);
-  Fe<P> Y3 = fe_sub_lz<2>(pf2_mul<P, BETA>(R, fe_sub_lz<2>(Q, X3)), pf2_mul<P, BETA>(a.y, PPP));  // < 4p
+  Fe<P> Y3;
+  if constexpr (TRIM && BETA == -1) {
+    // Y3 = R W - Y1 PPP (W = Q - X3) as ONE reduction of four products per lane:
+    //   lane 0: R0 W0 + Y1 P1 - R1 W1 - Y0 P0     lane 1: R1 W0 + R0 W1 - Y1 P0 - Y0 P1
+    const Fe<P> W = fe_sub_lz<2>(Q, X3);                                       // < 4p
+    const bool odd = pair_odd();
+    const Fe<P> Rp = fe_swap(R), Wp = fe_swap(W), Yp = fe_swap(a.y), Pp = fe_swap(PPP);
+    Y3 = fe_mul4_redc(R, fe_select(odd, Wp, W), fe_select(odd, Rp, Yp), fe_select(odd, W, Pp),
+                      fe_select(odd, a.y, Rp), fe_select(odd, Pp, Wp), fe_select(odd, Yp, a.y), PPP);  // < 2.3p
+  } else {
+    Y3 = fe_sub_lz<2>(pf2_mul<P, BETA>(R, fe_sub_lz<2>(Q, X3)), pf2_mul<P, BETA>(a.y, PPP));  // < 4p
+  }
   fe_to2p<4>(Y3);
   a.x = X3;
   a.y = Y3;
