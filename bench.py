@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--ntt-logn", type=int, default=24)
     ap.add_argument("--g16-logn", type=str, default="20,24", help="Groth16 prove domains, comma list ('' = skip)")
     ap.add_argument("--msm-extra", type=int, default=1, help="secondary G2 / BLS12-377 MSM lines (0 = skip)")
-    ap.add_argument("--g16-plain", type=str, default="20",
+    ap.add_argument("--g16-plain", type=str, default="20,24",
                     help="Groth16 domains also proved with a plain (non-precomputed) pk")
     ap.add_argument("--g16-sharded-logn", type=int, default=24,
                     help="N>1: sharded Groth16 prove domain (BASELINE config 4; 0 = skip)")

@@ -1,3 +1,5 @@
+//go:build icicle
+
 // Package gm is the cgo binding of libgnark_mi355x (include/gnark_mi355x.h)
 // shared by the gnark hooks in this directory (icicle_bn254, icicle_bls12377,
 // plonk_bls12377) and by the iciclegnark-compatible shim

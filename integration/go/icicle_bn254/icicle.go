@@ -18,6 +18,7 @@ package icicle_bn254
 
 import (
 	"fmt"
+	"math"
 	"math/big"
 	"os"
 	"unsafe"
@@ -102,10 +103,15 @@ func (pk *ProvingKey) setupDevicePointers(r1cs *cs.R1CS) error {
 		return err
 	}
 	pk.deviceInfo = &deviceInfo{key: key}
-	// the constraint system too (one GPU): proofs then send the wires alone
+	// the constraint system too (one GPU): proofs then send the wires alone.
+	// It is an optimisation: if it cannot be uploaded (device memory after a
+	// large precomputed key, term counts beyond u32) the proofs send a, b, c.
 	if gm.NbDevices() == 1 && os.Getenv("GNARK_MI355X_R1CS") != "0" {
-		if pk.deviceInfo.r1, err = uploadR1CS(r1cs); err != nil {
-			return err
+		r1, err := uploadR1CS(r1cs)
+		if err != nil {
+			logger.Logger().Warn().Err(err).Msg("mi355x: R1CS not resident, a/b/c are sent per proof")
+		} else {
+			pk.deviceInfo.r1 = r1
 		}
 	}
 	return nil
@@ -116,6 +122,9 @@ func (pk *ProvingKey) setupDevicePointers(r1cs *cs.R1CS) error {
 // GM_R1CS_CONST) and the CoeffTable to gm_r1cs_upload.
 func uploadR1CS(r1cs *cs.R1CS) (*gm.R1CS, error) {
 	rows := r1cs.GetR1Cs()
+	if len(rows) == 0 || len(r1cs.Coefficients) == 0 {
+		return nil, fmt.Errorf("empty constraint system")
+	}
 	var rowptr, cid, vid [3][]uint32
 	for m := 0; m < 3; m++ {
 		rowptr[m] = make([]uint32, 1, len(rows)+1)
@@ -125,6 +134,10 @@ func uploadR1CS(r1cs *cs.R1CS) (*gm.R1CS, error) {
 			for _, t := range l {
 				cid[m] = append(cid[m], t.CID)
 				vid[m] = append(vid[m], t.VID)
+			}
+			// the row pointers are u32 (gm_r1cs_upload)
+			if uint64(len(cid[m])) > math.MaxUint32 {
+				return nil, fmt.Errorf("matrix %d has more than 2^32-1 terms", m)
 			}
 			rowptr[m] = append(rowptr[m], uint32(len(cid[m])))
 		}
@@ -219,6 +232,21 @@ func Prove(r1cs *cs.R1CS, pk *ProvingKey, fullWitness witness.Witness, opts ...b
 		solver.OverrideHint(solver.GetHintID(fcs.Bsb22CommitmentComputePlaceholder),
 			bsb22Hint(pk, info, proof, committed, &opt)))
 
+	// -tags mi355x_levelhook: a, b, c move to the GPU level by level during
+	// Solve (staged.go); otherwise beginStaged returns nil (staged_off.go)
+	var staged *stagedRun
+	if pk.deviceInfo.r1 == nil && gm.NbDevices() == 1 {
+		st, hookOpt, err := pk.beginStaged(r1cs.GetNbConstraints())
+		if err != nil {
+			return nil, err
+		}
+		if st != nil {
+			defer st.free()
+			staged = st
+			solverOpts = append(solverOpts, hookOpt)
+		}
+	}
+
 	sol, err := r1cs.Solve(fullWitness, solverOpts...)
 	if err != nil {
 		return nil, err
@@ -240,6 +268,14 @@ func Prove(r1cs *cs.R1CS, pk *ProvingKey, fullWitness witness.Witness, opts ...b
 		return nil, err
 	}
 
+	if staged != nil { // a, b, c already on the device
+		if err := staged.prove(w, &r, &s, unsafe.Pointer(&proof.Ar), unsafe.Pointer(&proof.Bs),
+			unsafe.Pointer(&proof.Krs)); err != nil {
+			return nil, err
+		}
+		log.Debug().Msg("prover done")
+		return proof, nil
+	}
 	if pk.deviceInfo.r1 != nil { // a, b, c come from the resident R1CS
 		if err := pk.deviceInfo.key.ProveR1CS(pk.deviceInfo.r1, unsafe.Pointer(&w[0]), unsafe.Pointer(&r),
 			unsafe.Pointer(&s), unsafe.Pointer(&proof.Ar), unsafe.Pointer(&proof.Bs), unsafe.Pointer(&proof.Krs)); err != nil {

@@ -125,3 +125,267 @@ def test_gm_go_pins_every_host_key_pointer():
         seg = src[src.index(fn):]
         seg = seg[:seg.index("\n}\n")]
         assert "var pin runtime.Pinner" in seg and "defer pin.Unpin()" in seg and "k.cHost(&pin" in seg, fn
+
+
+# ---------------------------------------------------------------------------
+# Build-tag completeness: gnark's default build (no tags,
+# the reference CI `go test ./...`, .github/workflows/pr.yml:63-67) must compile
+# the replacement packages WITHOUT cgo, exactly like the reference's
+# provingkey.go:1-36 + noicicle.go:1-18; the icicle build must see one
+# definition of every exported name.
+# ---------------------------------------------------------------------------
+
+TAG_SETS = [frozenset(), frozenset({"icicle"}), frozenset({"icicle", "mi355x_levelhook"})]
+HOOK_PKGS = ("icicle_bn254", "icicle_bls12377")
+GNARK_PKGS = HOOK_PKGS + ("gm", "plonk_bls12377")
+
+
+def build_expr(src):
+    """The //go:build expression of a Go file (None = untagged)."""
+    for line in src.split("\n"):
+        s = line.strip()
+        if s.startswith("//go:build "):
+            return s[len("//go:build "):].strip()
+        if s.startswith("package "):
+            return None
+    return None
+
+
+def eval_build(expr, tags):
+    """Evaluate a //go:build expression (!, &&, ||, parentheses) for a tag set."""
+    if expr is None:
+        return True
+    toks = re.findall(r"\(|\)|!|&&|\|\||[A-Za-z0-9_.]+", expr)
+    pos = [0]
+
+    def peek():
+        return toks[pos[0]] if pos[0] < len(toks) else None
+
+    def take():
+        pos[0] += 1
+        return toks[pos[0] - 1]
+
+    def atom():
+        t = take()
+        if t == "!":
+            return not atom()
+        if t == "(":
+            v = orx()
+            assert take() == ")", expr
+            return v
+        return t in tags or t in ("linux", "amd64", "cgo", "gc")
+
+    def andx():
+        v = atom()
+        while peek() == "&&":
+            take()
+            v = atom() and v
+        return v
+
+    def orx():
+        v = andx()
+        while peek() == "||":
+            take()
+            v = andx() or v
+        return v
+
+    v = orx()
+    assert pos[0] == len(toks), expr
+    return v
+
+
+def strip_go(src):
+    """Source without comments and string / rune literals."""
+    src = re.sub(r"`[^`]*`", '""', src)
+    src = re.sub(r'"(\\.|[^"\\\n])*"', '""', src)
+    src = re.sub(r"'(\\.|[^'\\\n])+'", "0", src)
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return re.sub(r"//[^\n]*", "", src)
+
+
+def imports(src):
+    """Import paths of a Go file."""
+    out = re.findall(r'(?m)^import\s+(?:\w+\s+)?"([^"]+)"', src)
+    for block in re.findall(r"(?ms)^import \((.*?)^\)", src):
+        out += re.findall(r'"([^"]+)"', block)
+    return out
+
+
+def top_decls(src):
+    """Package-level declarations: names of funcs/types/consts/vars, and
+    methods as Recv.name."""
+    code = strip_go(src)
+    out = []
+    for m in re.finditer(r"(?m)^func\s+(?:\(\s*\w*\s*\*?(\w+)\s*\)\s*)?(\w+)", code):
+        out.append(m.group(1) + "." + m.group(2) if m.group(1) else m.group(2))
+    for kw in ("type", "const", "var"):
+        for m in re.finditer(r"(?m)^" + kw + r"\s+(\w+)", code):
+            out.append(m.group(1))
+        for block in re.findall(r"(?ms)^" + kw + r" \((.*?)^\)", code):
+            out += re.findall(r"(?m)^\t(\w+)", block)
+    return out
+
+
+def pkg_files(pkg):
+    d = os.path.join(GO_DIR, pkg)
+    return {f: open(os.path.join(d, f)).read() for f in sorted(os.listdir(d))
+            if f.endswith(".go") and not f.endswith("_test.go")}
+
+
+def included(pkg, tags):
+    return {f: s for f, s in pkg_files(pkg).items() if eval_build(build_expr(s), tags)}
+
+
+def test_build_expr_evaluator():
+    assert eval_build(None, set())
+    assert eval_build("!icicle", set()) and not eval_build("!icicle", {"icicle"})
+    assert eval_build("icicle && !mi355x_levelhook", {"icicle"})
+    assert not eval_build("icicle && !mi355x_levelhook", {"icicle", "mi355x_levelhook"})
+    assert eval_build("(a || b) && !c", {"b"}) and not eval_build("(a || b) && !c", {"b", "c"})
+
+
+def test_every_tag_set_defines_the_hook_api_once():
+    for pkg in HOOK_PKGS:
+        for tags in TAG_SETS:
+            files = included(pkg, tags)
+            seen = {}
+            for f, s in files.items():
+                for d in top_decls(s):
+                    assert d not in seen, f"{pkg} {sorted(tags)}: {d} declared in {seen[d]} and {f}"
+                    seen[d] = f
+            for name in ("HasIcicle", "Prove", "ProvingKey", "Setup", "DummySetup", "deviceInfo",
+                         "ProvingKey.FreeDevice"):
+                assert name in seen, f"{pkg} {sorted(tags)}: {name} undefined"
+            # one package clause for all included files
+            pk = {re.search(r"(?m)^package (\w+)", s).group(1) for s in files.values()}
+            assert pk == {pkg}, (pkg, pk)
+
+
+def test_untagged_build_has_no_cgo_and_no_gm():
+    for pkg in GNARK_PKGS:
+        for f, s in included(pkg, frozenset()).items():
+            imps = imports(s)
+            assert "C" not in imps, f"{pkg}/{f}: untagged build imports \"C\""
+            assert not any(i.endswith("/mi355x/gm") for i in imps), f"{pkg}/{f}: untagged build imports gm"
+            assert "gm." not in strip_go(s), f"{pkg}/{f}: untagged build uses gm."
+
+
+def test_names_used_are_declared_in_the_same_tag_set():
+    """A package-level name (or method) declared under one tag set and used by
+    a file of another set where it is not declared is a compile error."""
+    for pkg in GNARK_PKGS:
+        every = set()
+        for s in pkg_files(pkg).values():
+            every |= set(top_decls(s))
+        plain = {d for d in every if "." not in d}
+        methods = {d.split(".")[1] for d in every if "." in d}
+        for tags in TAG_SETS:
+            files = included(pkg, tags)
+            have = set()
+            for s in files.values():
+                have |= set(top_decls(s))
+            have_plain = {d for d in have if "." not in d}
+            have_methods = {d.split(".")[1] for d in have if "." in d}
+            for f, s in files.items():
+                code = strip_go(s)
+                for m in re.finditer(r"(?<![\w.])([A-Za-z_]\w*)\b", code):
+                    name = m.group(1)
+                    assert not (name in plain and name not in have_plain), \
+                        f"{pkg}/{f} {sorted(tags)}: uses {name}, not declared in this tag set"
+                for m in re.finditer(r"\.([a-z]\w*)\(", code):
+                    name = m.group(1)
+                    assert not (name in methods and name not in have_methods), \
+                        f"{pkg}/{f} {sorted(tags)}: calls method {name}, not declared in this tag set"
+
+
+def test_levelhook_diff_applies_to_the_reference_solver(tmp_path):
+    """integration/go/solver_levelhook.diff (the csolver.WithLevelHook the
+    staged prover needs) is a real patch: `patch --dry-run` applies it cleanly
+    to the reference's constraint/solver/options.go and constraint/{bn254,
+    bls12-377}/solver.go (copied to a temp dir; nothing under /root/reference
+    is written)."""
+    import shutil
+    import subprocess
+    import pytest
+    ref = "/root/reference"
+    diff = os.path.join(GO_DIR, "solver_levelhook.diff")
+    text = open(diff).read()
+    assert "func WithLevelHook(h LevelHook) Option" in text
+    assert text.count("solver.levelDone(level)") == 4  # both branches of run(), both curves
+    files = ["constraint/solver/options.go", "constraint/bn254/solver.go", "constraint/bls12-377/solver.go"]
+    if not all(os.path.exists(os.path.join(ref, f)) for f in files) or shutil.which("patch") is None:
+        pytest.skip("reference checkout or patch(1) not available")
+    for f in files:
+        (tmp_path / os.path.dirname(f)).mkdir(parents=True, exist_ok=True)
+        shutil.copy(os.path.join(ref, f), tmp_path / f)
+    r = subprocess.run(["patch", "-p1", "--dry-run", "-F0", "-i", diff], cwd=tmp_path, capture_output=True, text=True)
+    assert r.returncode == 0 and "FAILED" not in r.stdout and "fuzz" not in r.stdout, r.stdout + r.stderr
+    # the staged prover uses exactly the hook type the patch declares
+    staged = open(os.path.join(GO_DIR, "icicle_bn254", "staged.go")).read()
+    assert "csolver.WithLevelHook(hook)" in staged
+    assert "func(cIDs []uint32, a, b, c unsafe.Pointer)" in staged and \
+        "type LevelHook func(cIDs []uint32, a, b, c unsafe.Pointer)" in text
+
+
+def test_prove_diff_applies_to_the_reference_plonk_prover(tmp_path):
+    import shutil
+    import subprocess
+    import pytest
+    ref = "/root/reference/backend/plonk/bls12-377/prove.go"
+    diff = os.path.join(GO_DIR, "plonk_bls12377", "prove.go.diff")
+    if not os.path.exists(ref) or shutil.which("patch") is None:
+        pytest.skip("reference checkout or patch(1) not available")
+    dst = tmp_path / "backend/plonk/bls12-377"
+    dst.mkdir(parents=True)
+    shutil.copy(ref, dst / "prove.go")
+    r = subprocess.run(["patch", "-p1", "--dry-run", "-F0", "-i", diff], cwd=tmp_path, capture_output=True, text=True)
+    assert r.returncode == 0 and "FAILED" not in r.stdout and "fuzz" not in r.stdout, r.stdout + r.stderr
+
+
+def test_install_into_a_reference_checkout(tmp_path):
+    """integration/go/install.sh lays the seam into a copy of the reference
+    gnark tree and applies all three patches; in the installed tree the
+    untagged build of every touched package is cgo-free and the hook packages
+    define their API once per tag set (the checks above, on the real layout)."""
+    import shutil
+    import subprocess
+    import pytest
+    ref = "/root/reference"
+    if not os.path.exists(os.path.join(ref, "backend/groth16/groth16.go")) or shutil.which("patch") is None:
+        pytest.skip("reference checkout or patch(1) not available")
+    g = tmp_path / "gnark"
+    shutil.copytree(ref, g, ignore=shutil.ignore_patterns(".git"))
+    r = subprocess.run(["bash", os.path.join(GO_DIR, "install.sh"), str(g)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    src = (g / "backend/groth16/groth16.go").read_text()
+    assert "icicle_bls12377.Prove(_r1cs, pk.(*icicle_bls12377.ProvingKey)" in src
+    assert src.count("icicle_bls12377.HasIcicle") == 4  # Prove, Setup, DummySetup, NewProvingKey
+    assert "WithLevelHook" in (g / "constraint/solver/options.go").read_text()
+    for c in ("bn254", "bls12-377"):
+        assert "solver.levelDone(level)" in (g / "constraint" / c / "solver.go").read_text()
+    assert "s.commit(" in (g / "backend/plonk/bls12-377/prove.go").read_text()
+    gm = (g / "backend/accel/mi355x/gm/gm.go").read_text()
+    assert "#cgo CFLAGS: -I" + ROOT + "/include" in gm
+    dirs = {"icicle_bn254": "backend/groth16/bn254/icicle", "icicle_bls12377": "backend/groth16/bls12-377/icicle"}
+    for pkg, rel in dirs.items():
+        d = g / rel
+        names = sorted(f for f in os.listdir(d) if f.endswith(".go") and not f.endswith("_test.go"))
+        assert names == sorted(pkg_files(pkg)), (pkg, names)  # the stale reference files are gone
+        for tags in TAG_SETS:
+            seen = set()
+            for f in names:
+                s = (d / f).read_text()
+                if eval_build(build_expr(s), tags):
+                    for dcl in top_decls(s):
+                        assert dcl not in seen, (rel, sorted(tags), dcl)
+                        seen.add(dcl)
+            assert {"HasIcicle", "Prove", "ProvingKey", "Setup", "DummySetup", "deviceInfo"} <= seen
+    # the reference's own package test keeps compiling against the new key type
+    mt = (g / "backend/groth16/bn254/icicle/marshal_test.go").read_text()
+    assert "icicle_bn254.Setup(tCcs, &iciPK, &iciVK)" in mt
+    for rel in list(dirs.values()) + ["backend/accel/mi355x/gm", "backend/plonk/bls12-377"]:
+        for f in os.listdir(g / rel):
+            if f.endswith(".go"):
+                s = (g / rel / f).read_text()
+                if eval_build(build_expr(s), frozenset()):
+                    assert "C" not in imports(s) and not any(i.endswith("/mi355x/gm") for i in imports(s)), (rel, f)
