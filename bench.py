@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--msm-extra", type=int, default=1, help="secondary G2 / BLS12-377 MSM lines (0 = skip)")
     ap.add_argument("--g16-plain", type=str, default="20,24",
                     help="Groth16 domains also proved with a plain (non-precomputed) pk")
+    ap.add_argument("--g16-no-precomputed", action="store_true",
+                    help="prove only with the plain pk (profiling the default Go path)")
     ap.add_argument("--g16-sharded-logn", type=int, default=24,
                     help="N>1: sharded Groth16 prove domain (BASELINE config 4; 0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -300,7 +302,8 @@ def secondary(ctx, gm, args):
         for l in (int(x) for x in args.g16_logn.split(",") if x):
             if l in plain:
                 res["groth16"].append(groth16_bench(ctx, gm, l, precompute=False, check_oracle=(l <= 20)))
-            res["groth16"].append(groth16_bench(ctx, gm, l, precompute=True))
+            if not args.g16_no_precomputed:
+                res["groth16"].append(groth16_bench(ctx, gm, l, precompute=True))
     return res
 
 

@@ -14,6 +14,7 @@
 // low -> high with the twiddle before.  Three passes cover 2^24 (8+8+8), i.e.
 // three HBM round trips instead of 24.
 #include <cstdlib>
+#include <type_traits>
 
 #include "curves.hpp"
 #include "ntt.hpp"
@@ -258,6 +259,226 @@ __global__ void __launch_bounds__(TPB) k_ntt_pass(Fe<P>* __restrict__ data, int 
     }
     st_fe(data, addr, v);
   }
+}
+
+// ---------------------------------------------------------------------------
+// Radix-4 pass (default for t >= 2): the same pass as k_ntt_pass, but every
+// thread keeps four tile elements in registers and runs TWO radix-2 stages on
+// them between LDS exchanges.  A tile of 1024 elements is 256 groups of four:
+// round r takes elements j0 + {0, s, 2s, 3s} of column ol (quarter spacing
+// s = 2^ls, j0 = grp * 4s + jj, jj < s), so
+//   * the first round loads straight from HBM (fused pb/pc, pre and DIT twiddle)
+//     and the last round stores straight to HBM: the tile crosses LDS t/2 - 1
+//     times instead of t + 1 (t = 8: 3 exchanges instead of 9, 6 barriers
+//     instead of 9);
+//   * each round is four butterflies = four independent-ish product chains per
+//     thread (two per stage) and only three twiddle loads (w_2m^jj, w_2m^(jj+s),
+//     w_m^jj for DIF);
+//   * rounds whose twiddles are 1 and w_4 (s = 1: the last DIF round, the first
+//     DIT round) do one product instead of four, block-uniformly.
+// An odd t leaves one radix-2 stage, run on the LDS tile at the end (DIF lm = 0,
+// DIT lm = t - 1) exactly as in k_ntt_pass.
+// Bounds: DIF round inputs < 2p, outputs < 2p (two of the four sums reduced),
+// except the s = 1 round, whose outputs (< 8p) go straight to the store; DIT
+// (Harvey) round inputs < 4p, outputs < 4p.  Intermediate DIT passes store
+// lazily reduced (< 4p < 2^256; the next pass multiplies on load).
+// ---------------------------------------------------------------------------
+// f(0), f(1), f(2), f(3) with compile-time indices (register-resident arrays)
+template <class F>
+GM_DEV void unroll4(F&& f) {
+  f(std::integral_constant<int, 0>());
+  f(std::integral_constant<int, 1>());
+  f(std::integral_constant<int, 2>());
+  f(std::integral_constant<int, 3>());
+}
+
+template <class P>
+GM_DEV Fe<P> ntt_tw(const Fe<P>* __restrict__ sub, int i) {
+  return sub[i];
+}
+
+// DIF radix-2 butterfly pair of one round: (u, v) -> (u + v, (u - v + Kp) w)
+template <class P>
+GM_DEV void r4_dif(Fe<P> (&e)[4], const Fe<P>& t1, const Fe<P>& t2, const Fe<P>& t3) {
+  // stage lm: (e0, e2) by w_2m^jj, (e1, e3) by w_2m^(jj+s); inputs < 2p
+  const Fe<P> s0 = fe_add_lz(e[0], e[2]);                        // < 4p
+  const Fe<P> d0 = fe_mul_lz(fe_sub_lz<2>(e[0], e[2]), t1);      // < 2p
+  const Fe<P> s1 = fe_add_lz(e[1], e[3]);                        // < 4p
+  const Fe<P> d1 = fe_mul_lz(fe_sub_lz<2>(e[1], e[3]), t2);      // < 2p
+  // stage lm - 1: (s0, s1), (d0, d1) by w_m^jj
+  e[0] = fe_add_lz(s0, s1);                                      // < 8p
+  fe_reduce_k<4>(e[0]);
+  fe_reduce_k<2>(e[0]);                                          // < 2p
+  e[1] = fe_mul_lz(fe_sub_lz<4>(s0, s1), t3);                    // < 2p
+  e[2] = fe_add_lz(d0, d1);                                      // < 4p
+  fe_reduce_k<2>(e[2]);                                          // < 2p
+  e[3] = fe_mul_lz(fe_sub_lz<2>(d0, d1), t3);                    // < 2p
+}
+// the s = 1 DIF round (twiddles 1, w_4, 1): inputs < 2p, outputs < 8p
+template <class P>
+GM_DEV void r4_dif_w4(Fe<P> (&e)[4], const Fe<P>& w4) {
+  const Fe<P> s0 = fe_add_lz(e[0], e[2]);                        // < 4p
+  const Fe<P> d0 = fe_sub_lz<2>(e[0], e[2]);                     // < 4p
+  const Fe<P> s1 = fe_add_lz(e[1], e[3]);                        // < 4p
+  const Fe<P> d1 = fe_mul_lz(fe_sub_lz<2>(e[1], e[3]), w4);      // < 2p
+  e[0] = fe_add_lz(s0, s1);                                      // < 8p
+  e[1] = fe_sub_lz<4>(s0, s1);                                   // < 8p
+  e[2] = fe_add_lz(d0, d1);                                      // < 6p
+  e[3] = fe_sub_lz<2>(d0, d1);                                   // < 6p
+}
+// DIT (Harvey) round: (u, v) -> (u + v w, u - v w + 2p); inputs < 4p, outputs < 4p
+template <class P>
+GM_DEV void r4_dit(Fe<P> (&e)[4], const Fe<P>& a, const Fe<P>& b, const Fe<P>& c) {
+  // stage lm: (e0, e1), (e2, e3) by w_2m^jj
+  fe_reduce_k<2>(e[0]);
+  fe_reduce_k<2>(e[2]);
+  const Fe<P> v1 = fe_mul_lz(e[1], a);                           // < 2p
+  const Fe<P> v3 = fe_mul_lz(e[3], a);
+  Fe<P> s0 = fe_add_lz(e[0], v1);                                // < 4p
+  Fe<P> s1 = fe_sub_lz<2>(e[0], v1);
+  const Fe<P> s2 = fe_add_lz(e[2], v3);
+  const Fe<P> s3 = fe_sub_lz<2>(e[2], v3);
+  // stage lm + 1: (s0, s2) by w_4m^jj, (s1, s3) by w_4m^(jj+s)
+  fe_reduce_k<2>(s0);
+  fe_reduce_k<2>(s1);
+  const Fe<P> x = fe_mul_lz(s2, b);
+  const Fe<P> y = fe_mul_lz(s3, c);
+  e[0] = fe_add_lz(s0, x);
+  e[2] = fe_sub_lz<2>(s0, x);
+  e[1] = fe_add_lz(s1, y);
+  e[3] = fe_sub_lz<2>(s1, y);
+}
+// the s = 1 DIT round (twiddles 1, 1, w_4): inputs < 2p, outputs < 4p
+template <class P>
+GM_DEV void r4_dit_w4(Fe<P> (&e)[4], const Fe<P>& w4) {
+  const Fe<P> s0 = fe_add_lz(e[0], e[1]);                        // < 4p
+  const Fe<P> s1 = fe_sub_lz<2>(e[0], e[1]);                     // < 4p
+  const Fe<P> s2 = fe_add_lz(e[2], e[3]);                        // < 4p
+  const Fe<P> y = fe_mul_lz(fe_sub_lz<2>(e[2], e[3]), w4);       // < 2p
+  e[0] = fe_add_lz(s0, s2);                                      // < 8p
+  e[2] = fe_sub_lz<4>(s0, s2);                                   // < 8p
+  e[1] = fe_add_lz(s1, y);                                       // < 6p
+  e[3] = fe_sub_lz<2>(s1, y);                                    // < 6p
+  unroll4([&](auto I) { fe_reduce_k<4>(e[I]); });               // < 4p
+}
+
+template <class P, bool DIT>
+__global__ void __launch_bounds__(NTT_TPB) k_ntt_pass4(Fe<P>* __restrict__ data, int logn, int lo, int t,
+                                                       const Fe<P>* __restrict__ tw,
+                                                       const Fe<P>* __restrict__ sub,
+                                                       const Fe<P>* __restrict__ pre,
+                                                       const Fe<P>* __restrict__ post,
+                                                       const Fe<P>* __restrict__ pb,
+                                                       const Fe<P>* __restrict__ pc) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  Fe<P>* X = reinterpret_cast<Fe<P>*>(smem_raw);  // [T][B]
+  const int T = 1 << t;
+  const int lgB = NTT_TILE_LOG - t;
+  const int B = 1 << lgB;
+  const size_t nother = (size_t)1 << (logn - t);
+  const int ol = threadIdx.x & (B - 1);
+  const int k = threadIdx.x >> lgB;  // group of the column: [0, T/4)
+  const size_t o = (size_t)blockIdx.x * B + ol;
+  const bool live = o < nother;
+  const size_t lomask = ((size_t)1 << lo) - 1;
+  const size_t base = ((o >> lo) << (lo + t)) + (o & lomask);  // (j, ol) lives at base + (j << lo)
+  const bool last_pass = DIT ? (lo + t == logn) : (lo == 0);
+  // rounds: DIF stages (t-1, t-2), (t-3, t-4), ...; DIT (0, 1), (2, 3), ...
+  const int nr = t >> 1;
+  auto quarter = [&](int r) { return DIT ? 2 * r : t - 2 - 2 * r; };  // ls of round r
+  Fe<P> e[4];
+  int j0 = 0, s = 0;
+  auto place = [&](int r) {
+    const int ls = quarter(r);
+    s = 1 << ls;
+    j0 = ((k >> ls) << (ls + 2)) + (k & (s - 1));
+  };
+  place(0);
+  if (live) {
+    unroll4([&](auto I) {
+      const size_t addr = base + ((size_t)(j0 + I * s) << lo);
+      Fe<P> v = ld_fe(data, addr);
+      if (pb) v = fe_sub(fe_mul(v, fe_to_internal(ld_fe(pb, addr))), ld_fe(pc, addr));
+      if (pre) v = fe_mul(v, ld_tab(pre, addr));
+      if (DIT && lo > 0) v = fe_mul_lz(v, ld_tab(tw, ((size_t)(j0 + I * s) << lo) + (o & lomask)));  // < 2p
+      e[I] = v;
+    });
+  }
+  for (int r = 0; r < nr; r++) {
+    if (r > 0) {
+      // exchange through the tile: this round's elements of every thread
+      __syncthreads();  // the previous round's reads are done
+      unroll4([&](auto I) { X[(j0 + I * s) * B + ol] = e[I]; });
+      __syncthreads();
+      place(r);
+      unroll4([&](auto I) { e[I] = X[(j0 + I * s) * B + ol]; });
+    }
+    const int ls = quarter(r);
+    const int jj = k & (s - 1);
+    if (s == 1) {  // block-uniform
+      const Fe<P> w4 = ntt_tw(sub, 1 << (t - 2));
+      if (DIT) r4_dit_w4(e, w4);
+      else r4_dif_w4(e, w4);
+    } else if (!DIT) {
+      r4_dif(e, ntt_tw(sub, jj << (t - ls - 2)), ntt_tw(sub, (jj + s) << (t - ls - 2)), ntt_tw(sub, jj << (t - ls - 1)));
+    } else {
+      r4_dit(e, ntt_tw(sub, jj << (t - ls - 1)), ntt_tw(sub, jj << (t - ls - 2)), ntt_tw(sub, (jj + s) << (t - ls - 2)));
+    }
+  }
+  if (t & 1) {
+    // the lone radix-2 stage on the tile (DIF lm = 0 after the rounds: inputs
+    // < 2p; DIT lm = t - 1: inputs < 4p), then the store from LDS
+    __syncthreads();
+    unroll4([&](auto I) { X[(j0 + I * s) * B + ol] = e[I]; });
+    __syncthreads();
+    const int lm = DIT ? t - 1 : 0;
+    const int m = 1 << lm, step = T >> (lm + 1);
+    for (int q = threadIdx.x; q < NTT_TILE / 2; q += NTT_TPB) {
+      int jj, bol, grp;
+      bfly_index(q, lm, lgB, jj, bol, grp);
+      const int a0 = ((grp << (lm + 1)) + jj) * B + bol, a1 = a0 + m * B;
+      Fe<P> u = X[a0], v = X[a1];
+      if (!DIT) {
+        Fe<P> sm = fe_add_lz(u, v);
+        fe_reduce_k<2>(sm);
+        Fe<P> d = fe_sub_lz<2>(u, v);
+        if (lm >= 1) d = fe_mul_lz(d, ntt_tw(sub, jj * step));
+        else fe_reduce_k<2>(d);
+        X[a0] = sm;
+        X[a1] = d;
+      } else {
+        fe_reduce_k<2>(u);
+        if (jj || lm >= 2) v = fe_mul_lz(v, ntt_tw(sub, jj * step));
+        else fe_reduce_k<2>(v);
+        X[a0] = fe_add_lz(u, v);
+        X[a1] = fe_sub_lz<2>(u, v);
+      }
+    }
+    __syncthreads();
+    unroll4([&](auto I) { e[I] = X[(j0 + I * s) * B + ol]; });  // < 2p (DIF) / < 4p (DIT)
+  }
+  if (!live) return;
+  // store: the last round's (or the re-read lone-stage) elements.  Bounds here:
+  // DIF < 8p (s = 1 round) or < 2p; DIT < 4p.
+  const bool wide = !DIT && s == 1 && !(t & 1);
+  unroll4([&](auto I) {
+    const int j = j0 + I * s;
+    const size_t addr = base + ((size_t)j << lo);
+    Fe<P> v = e[I];
+    if (!DIT && lo > 0) {
+      // inter-pass twiddle of a DIF pass (never the last pass): stored < 2p
+      v = fe_mul_lz(v, ld_tab(tw, ((size_t)j << lo) + (o & lomask)));
+    } else if (post) {
+      v = fe_mul(v, ld_tab(post, addr));  // inputs < 8p: (8p) p < R' p, output canonical
+    } else if (DIT && !last_pass) {
+      // lazily reduced (< 4p < 2^256): the next DIT pass multiplies it on load
+    } else {
+      if (wide) fe_reduce_k<4>(v);
+      fe_reduce_k<2>(v);
+      fe_reduce_once(v);
+    }
+    st_fe(data, addr, v);
+  });
 }
 
 // ---------------------------------------------------------------------------
@@ -575,6 +796,8 @@ static int run_passes(gm_ctx* ctx, NttDomain<C>* d, Fe<typename C::Fr>* a, bool 
   // GM_NTT_TPB=512: one butterfly per thread and stage (no gain measured).
   static const int tpb = getenv("GM_NTT_TPB") ? atoi(getenv("GM_NTT_TPB")) : NTT_TPB;
   static const bool swg = getenv("GM_NTT_SWG") ? atoi(getenv("GM_NTT_SWG")) != 0 : true;
+  // radix-4 passes (k_ntt_pass4) by default; GM_NTT_R4=0: the radix-2 kernel (A/B)
+  static const bool r4 = getenv("GM_NTT_R4") ? atoi(getenv("GM_NTT_R4")) != 0 : true;
   const size_t smem = sizeof(Fe<Fr>) * (NTT_TILE + (swg ? 0 : (1 << (NTT_TMAX - 1))));
   const int np = (int)d->passes.size();
   for (int k = 0; k < np; k++) {
@@ -588,6 +811,13 @@ static int run_passes(gm_ctx* ctx, NttDomain<C>* d, Fe<typename C::Fr>* a, bool 
     const size_t B = NTT_TILE >> ps.t;
     const unsigned grid = (unsigned)((nother + B - 1) / B);
     ProfScope pscope(ctx, "ntt_pass");
+    if (r4 && ps.t >= 2) {
+      auto k4 = dit ? k_ntt_pass4<Fr, true> : k_ntt_pass4<Fr, false>;
+      hipLaunchKernelGGL(k4, dim3(grid), dim3(NTT_TPB),
+                         sizeof(Fe<Fr>) * NTT_TILE, st, a, d->logn, ps.lo, ps.t, tw, sub, first ? fz.pre : nullptr,
+                         last ? fz.post : nullptr, first ? fz.pb : nullptr, first ? fz.pc : nullptr);
+      continue;
+    }
     auto kern = dit ? k_ntt_pass<Fr, true> : k_ntt_pass<Fr, false>;
     if (tpb == 512) kern = dit ? (swg ? k_ntt_pass<Fr, true, 512, true> : k_ntt_pass<Fr, true, 512>)
                                : (swg ? k_ntt_pass<Fr, false, 512, true> : k_ntt_pass<Fr, false, 512>);

@@ -210,3 +210,29 @@ def test_groth16_2p24_synthetic_pk(gm_ctx, oracle):
             dpk.free()
         assert got == exp, precompute
         _log("gpu prove (precompute=%s) matches" % precompute)
+    # configs[3]'s own form: the same 2^24 key as world = 8 shards (one GPU
+    # plays every rank in turn): each rank's slice (gm_g16_pk_upload_shard),
+    # its five partial sums (gm_g16_prove_partial), host-reduced and finished
+    # (gm_g16_finish) -- byte-identical to the same oracle proof
+    world = 8
+    dev = [gm_ctx.copy_to_device(W)] + [gm_ctx.malloc(32 * n) for _ in range(3)]
+    parts = []
+    hpk = {k: v for k, v in pk.items() if k != "sizes"}
+    try:
+        for rank in range(world):
+            dpk = gm.ProvingKey(gm_ctx, cname, hpk, n, nb_wires, nb_public, precompute=(rank % 2 == 1),
+                                shard=(rank, world))
+            try:
+                for buf, v in zip(dev[1:], (a, b, cc)):  # computeH overwrites a, b, c: fresh per rank
+                    buf.write(bytes(32 * n))
+                    buf.write(v)
+                parts.append(dpk.prove_partial_device(dev[0], dev[1], dev[2], dev[3], nc))
+                if rank == world - 1:
+                    got = gm.g16_finish(cname, dpk._h, gm.g16_reduce_partials(cname, parts), rb, sb)
+            finally:
+                dpk.free()
+    finally:
+        for x in dev:
+            x.free()
+    assert got == exp
+    _log("sharded world=8 prove matches")

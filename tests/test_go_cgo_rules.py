@@ -363,7 +363,7 @@ def test_install_into_a_reference_checkout(tmp_path):
     assert "WithLevelHook" in (g / "constraint/solver/options.go").read_text()
     for c in ("bn254", "bls12-377"):
         assert "solver.levelDone(level)" in (g / "constraint" / c / "solver.go").read_text()
-    assert "s.commit(" in (g / "backend/plonk/bls12-377/prove.go").read_text()
+    assert "s.commitLagrange(" in (g / "backend/plonk/bls12-377/prove.go").read_text()
     gm = (g / "backend/accel/mi355x/gm/gm.go").read_text()
     assert "#cgo CFLAGS: -I" + ROOT + "/include" in gm
     dirs = {"icicle_bn254": "backend/groth16/bn254/icicle", "icicle_bls12377": "backend/groth16/bls12-377/icicle"}

@@ -232,3 +232,52 @@ def test_oracle_signed_pippenger_vs_unsigned(oracle, cname, g2):
         pts = oracle.batch_mul_base(cname, g2, oracle.generator(cname, g2),
                                     R.encode_vec(cname, pyref.random_scalars(c, n, n + 12)))
         assert oracle.msm(cname, g2, sb, pts) == oracle.msm(cname, g2, sb, pts, naive=2), n
+
+
+def _glv_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "glv_constants", os.path.join(HERE, "..", "tools", "glv_constants.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def _hpp_array(name, struct):
+    """The uint32 array literal of `name` inside `struct` in csrc/msm_impl.hpp."""
+    import re
+    src = open(os.path.join(HERE, "..", "gnark-icicle_amd", "csrc", "msm_impl.hpp")).read()
+    body = src[src.index("struct %s {" % struct):]
+    body = body[:body.index("\n};")]
+    fn = body[body.index(name + "(int i)"):]
+    lit = fn[fn.index("{", fn.index("a[")) + 1:fn.index("};")]
+    return [int(x.rstrip("u"), 16) for x in re.findall(r"0x[0-9a-fA-F]+u", lit)]
+
+
+def test_bn254_glv_constants_pinned_by_reference():
+    """The BN254 GLV endomorphism of the MSM (csrc/msm_impl.hpp GlvBn254) is the
+    conjugate of the one the reference holds: std/algebra/emulated/sw_emulated/
+    params.go:54-55 (GetBN254Params: Eigenvalue lambda_ref, ThirdRootOne
+    omega_ref).  Ours: lambda = r - 1 - lambda_ref = lambda_ref^2 mod r and
+    beta = p - 1 - omega_ref = omega_ref^2 mod p; both pairs satisfy
+    phi(x, y) = (beta x, y) = [lambda](x, y) on G1, and the device's radix-2^29
+    Montgomery beta (and beta^2 for the G2 twist) encode exactly these."""
+    c = pyref.BN254
+    p, r = c.p, c.r
+    lam_ref = 4407920970296243842393367215006156084916469457145843978461
+    omega_ref = 2203960485148121921418603742825762020974279258880205651966
+    d = _glv_module().derive()
+    assert d["lam"] == r - 1 - lam_ref == lam_ref * lam_ref % r
+    assert d["beta"] == p - 1 - omega_ref == omega_ref * omega_ref % p
+    G = pyref.Group(c, False)
+    P = G.mul(G.generator(), 0x1234567)
+    assert G.mul(P, lam_ref) == (omega_ref * P[0] % p, P[1])      # the reference's pair
+    assert G.mul(P, d["lam"]) == (d["beta"] * P[0] % p, P[1])      # the device's (conjugate) pair
+
+    def r29(x):
+        v = x * (1 << 261) % p
+        return [(v >> (29 * i)) & ((1 << 29) - 1) for i in range(9)]
+    assert _hpp_array("beta29", "GlvBn254") == r29(d["beta"])
+    assert _hpp_array("beta29_g2", "GlvBn254") == r29(d["beta"] * d["beta"] % p)
+    # the lattice basis the device splits with: a + b lambda = 0 mod r
+    assert (d["a1"] + d["b1"] * d["lam"]) % r == 0 and (d["a2"] + d["b2"] * d["lam"]) % r == 0

@@ -100,3 +100,111 @@ def test_plonk_bls12377_commit_fft_replay(gm_ctx, oracle, logn):
     finally:
         d_canon.free()
         d_lagr.free()
+
+
+def _quotient(r, f, fz, z):
+    """(f(X) - fz) / (X - z) by synthetic division, as kzg_mi355x.go's
+    quotientByXminusZ (gnark-crypto kzg's dividePolyByXminusA)."""
+    f = list(f)
+    f[0] = (f[0] - fz) % r
+    for i in range(len(f) - 2, -1, -1):
+        f[i] = (f[i] + f[i + 1] * z) % r
+    return f[1:]
+
+
+def _eval(r, f, z):
+    acc = 0
+    for a in reversed(f):
+        acc = (acc * z + a) % r
+    return acc
+
+
+@pytest.mark.parametrize("logn", [6, 10])
+def test_plonk_bls12377_openings_and_domain0_replay(gm_ctx, oracle, logn):
+    """The remaining n-size MSMs and FFTs of the patched prover (prove.go.diff):
+      openZ :611             kzg.Open(blindedZ, zeta*w) -> s.open: claimed value
+                             (Horner), quotient (synthetic division) on the host,
+                             commit(quotient, pk.Kzg) on the GPU
+      batchOpening :757      kzg.BatchOpenSinglePoint -> s.batchOpen: the folded
+                             polynomial sum gamma^i f_i, its quotient, GPU commit
+      computeNumerator :949, :967, :1016 and :1301
+                             domain0 ToCanonical (Lagrange Regular -> FFTInverse
+                             DIF -> Canonical BitReverse), scaling, ToLagrange
+                             (Canonical BitReverse -> FFT DIT -> Lagrange Regular)
+    Each commit is checked against the oracle MSM AND against the KZG identity
+    commit(q) = [(f(tau) - f(z)) / (tau - z)] G1, which pins the quotient itself
+    (tau is known to the test)."""
+    import gnark_mi355x as gm
+    c = pyref.CURVES[CNAME]
+    r = c.r
+    n = 1 << logn
+    enc = lambda vals: b"".join(pyref.encode_fr(c, v) for v in vals)
+    dec = lambda b: [pyref.decode_fr(c, b[32 * i:32 * i + 32]) for i in range(len(b) // 32)]
+    tau = pyref.random_scalars(c, 1, 0x79)[0]
+    canon, _ = _srs(oracle, gm, n, tau)
+    d_canon = gm_ctx.points_upload(CNAME, canon)
+    gen = gm.generator(CNAME)
+    G = pyref.Group(c, False)
+
+    def commit_checked(q, what):
+        got = gm_ctx.kzg_commit(CNAME, d_canon, enc(q))
+        assert got == oracle.msm(CNAME, False, enc(q), canon[:gm.point_bytes(CNAME, False) * len(q)]), what
+        return got
+
+    try:
+        # openZ (:611): blinded Z has n + 3 coefficients (the SRS size)
+        z = pyref.random_scalars(c, 1, 0x80)[0]
+        bz = pyref.random_scalars(c, n + 3, 0x81)
+        v = _eval(r, bz, z)
+        q = _quotient(r, bz, v, z)
+        assert len(q) == n + 2
+        got = commit_checked(q, "open")
+        want = oracle.batch_mul_base(CNAME, False, gen, enc([(_eval(r, bz, tau) - v) * pow(tau - z, -1, r) % r]))
+        assert got == want, "open: quotient commitment != [(f(tau) - f(z)) / (tau - z)] G"
+        # batchOpening (:757): six polynomials of different lengths, one gamma
+        gamma = pyref.random_scalars(c, 1, 0x82)[0]
+        lens = [n + 2, n + 3, n + 3, n + 3, n, n]
+        polys = [pyref.random_scalars(c, m, 0x90 + i) for i, m in enumerate(lens)]
+        claimed = [_eval(r, f, z) for f in polys]
+        folded = [0] * max(lens)
+        gi = 1
+        for f in polys:
+            for j, a in enumerate(f):
+                folded[j] = (folded[j] + gi * a) % r
+            gi = gi * gamma % r
+        fz = 0
+        for v_ in reversed(claimed):
+            fz = (fz * gamma + v_) % r
+        assert fz == _eval(r, folded, z)
+        q = _quotient(r, folded, fz, z)
+        got = commit_checked(q, "batch open")
+        want = oracle.batch_mul_base(CNAME, False, gen, enc([(_eval(r, folded, tau) - fz) * pow(tau - z, -1, r) % r]))
+        assert got == want, "batch open: quotient commitment mismatch"
+        # computeNumerator (:949-967) on domain0, one polynomial through the GPU
+        lag = enc(pyref.random_scalars(c, n, 0xA0))
+        X = gm_ctx.copy_to_device(lag)
+        gm_ctx.ntt(CNAME, X, n, True, False, False)  # ToCanonical: FFTInverse(DIF), Regular -> BitReverse
+        canon_brev = X.to_host()
+        assert canon_brev == oracle.fft(CNAME, lag, True, False, False)
+        # the coefficients really are p's canonical ones, bit-reversed
+        co = dec(canon_brev)
+        nat = [co[pyref.bitrev(i, logn)] for i in range(n)]
+        w0 = pyref.domain_generator(c, n)
+        lv = dec(lag)
+        for i in (0, 1, n - 1):
+            assert _eval(r, nat, pow(w0, i, r)) == lv[i]
+        # scale by the bit-reversed scaling vector (host, as prove.go:952-963), ToLagrange: FFT(DIT) -> Regular
+        shift = pyref.random_scalars(c, 1, 0xA1)[0]
+        sv = [pow(shift, pyref.bitrev(i, logn), r) for i in range(n)]
+        scaled = enc([a * b % r for a, b in zip(co, sv)])
+        X.write(scaled)
+        gm_ctx.ntt(CNAME, X, n, False, True, False)
+        assert X.to_host() == oracle.fft(CNAME, scaled, False, True, False)
+        # :1016 / :1301: ToCanonical of a Lagrange BitReverse polynomial -> FFTInverse(DIT) -> Regular
+        lag_br = enc(pyref.random_scalars(c, n, 0xA2))
+        X.write(lag_br)
+        gm_ctx.ntt(CNAME, X, n, True, True, False)
+        assert X.to_host() == oracle.fft(CNAME, lag_br, True, True, False)
+        X.free()
+    finally:
+        d_canon.free()

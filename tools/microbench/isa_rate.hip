@@ -10,6 +10,7 @@ template <int OP, bool LAT = false>
 __global__ void __launch_bounds__(256) kop(uint32_t* out, int iters) {
   uint64_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
   uint32_t x = threadIdx.x * 3 + 1, y = threadIdx.x * 7 + 5;
+  uint64_t fx = 0x3ff0000000000000ull + threadIdx.x, fy = 0x3ff0000000000001ull;  // doubles near 1.0
   for (int k = 0; k < iters; k++) {
 #define BODY(A)                                                                                  \
   if constexpr (OP == 0) { uint64_t cc_; asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(A), "=s"(cc_) : "v"(x), "v"(y)); } \
@@ -18,7 +19,13 @@ __global__ void __launch_bounds__(256) kop(uint32_t* out, int iters) {
   if constexpr (OP == 3) asm volatile("v_and_b32 %0, %0, %1" : "+v"(*(uint32_t*)&A) : "v"(y));    \
   if constexpr (OP == 4) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(*(uint32_t*)&A) : "v"(x), "v"(y)); \
   if constexpr (OP == 5) asm volatile("v_lshl_add_u64 %0, %0, 1, %0" : "+v"(A));                  \
-  if constexpr (OP == 6) asm volatile("v_alignbit_b32 %0, %0, %1, 29" : "+v"(*(uint32_t*)&A) : "v"(y));
+  if constexpr (OP == 6) asm volatile("v_alignbit_b32 %0, %0, %1, 29" : "+v"(*(uint32_t*)&A) : "v"(y));    \
+  if constexpr (OP == 7) asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(A) : "v"(fx), "v"(fy));      \
+  if constexpr (OP == 8) asm volatile("v_add_f64 %0, %0, %1" : "+v"(A) : "v"(fx));                    \
+  if constexpr (OP == 9) asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(*(uint32_t*)&A) : "v"(y));     \
+  if constexpr (OP == 10) asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(*(uint32_t*)&A) : "v"(y));   \
+  if constexpr (OP == 11) { uint64_t cc_; asm volatile("v_add_co_u32 %0, %1, %0, %2" : "+v"(*(uint32_t*)&A), "=s"(cc_) : "v"(y)); } \
+  if constexpr (OP == 12) asm volatile("v_add_u32 %0, %0, %1" : "+v"(*(uint32_t*)&A) : "v"(y));
     if constexpr (LAT) {
       REP8(BODY(a0) BODY(a0) BODY(a0) BODY(a0) BODY(a0) BODY(a0) BODY(a0) BODY(a0))
     } else {
@@ -30,7 +37,8 @@ __global__ void __launch_bounds__(256) kop(uint32_t* out, int iters) {
 }
 
 static const char* NAMES[] = {"v_mad_u64_u32", "v_lshrrev_b64", "v_mul_lo_u32", "v_and_b32",
-                              "v_add3_u32", "v_lshl_add_u64", "v_alignbit_b32"};
+                              "v_add3_u32", "v_lshl_add_u64", "v_alignbit_b32", "v_fma_f64", "v_add_f64",
+                              "v_mul_hi_u32", "v_mul_u32_u24", "v_add_co_u32", "v_add_u32"};
 
 template <int OP, bool LAT = false>
 void run(uint32_t* d, int cus, double ghz) {
@@ -65,6 +73,13 @@ int main() {
   run<4>(d, p.multiProcessorCount, ghz);
   run<5>(d, p.multiProcessorCount, ghz);
   run<6>(d, p.multiProcessorCount, ghz);
+  run<7>(d, p.multiProcessorCount, ghz);
+  run<8>(d, p.multiProcessorCount, ghz);
+  run<9>(d, p.multiProcessorCount, ghz);
+  run<10>(d, p.multiProcessorCount, ghz);
+  run<11>(d, p.multiProcessorCount, ghz);
+  run<12>(d, p.multiProcessorCount, ghz);
+  run<7, true>(d, p.multiProcessorCount, ghz);
   run<0, true>(d, p.multiProcessorCount, ghz);
   run<1, true>(d, p.multiProcessorCount, ghz);
   run<3, true>(d, p.multiProcessorCount, ghz);
