@@ -263,7 +263,12 @@ GM_DEV Fe<P> fe_neg(const Fe<P>& a) {
 // column k accumulates a_i b_{k-i} + m_i p_{k-i} (< 2N * 2^58 < 2^64) in one
 // 64-bit register; m_k = (acc * (-p^-1)) mod 2^29 zeroes the low limb.
 // Inputs < p  ->  result < 2p -> one conditional subtraction -> canonical.
-template <class P, bool REDUCE = true>
+// CHAIN: every column starts from the carry of the previous one (an opaque
+// register barrier stops the compiler from summing the next column separately
+// and adding the carry with a 64-bit add, v_lshl_add_u64, per column).  One
+// dependent mad chain per product: for kernels with several independent
+// products in flight per thread (the radix-4 NTT rounds).
+template <class P, bool REDUCE = true, bool CHAIN = false>
 GM_DEV Fe<P> fe_mul(const Fe<P>& a, const Fe<P>& b) {
   constexpr int N = P::N;
   uint32_t m[N];
@@ -271,6 +276,9 @@ GM_DEV Fe<P> fe_mul(const Fe<P>& a, const Fe<P>& b) {
   uint64_t acc = 0;
 #pragma unroll
   for (int k = 0; k < 2 * N - 1; k++) {
+    if constexpr (CHAIN) {
+      if (k) __asm__ volatile("" : "+v"(acc));
+    }
 #pragma unroll
     for (int i = (k - N + 1 > 0 ? k - N + 1 : 0); i <= (k < N - 1 ? k : N - 1); i++)
       acc += (uint64_t)a.v[i] * b.v[k - i];
@@ -358,6 +366,8 @@ GM_HD constexpr uint32_t kp_top(int j) {
 }
 template <class P>
 GM_DEV Fe<P> fe_mul_lz(const Fe<P>& a, const Fe<P>& b) { return fe_mul<P, false>(a, b); }
+template <class P>
+GM_DEV Fe<P> fe_mul_lz_chain(const Fe<P>& a, const Fe<P>& b) { return fe_mul<P, false, true>(a, b); }
 template <class P>
 GM_DEV Fe<P> fe_sqr_lz(const Fe<P>& a) { return fe_sqr<P, false>(a); }
 // Montgomery reduction of x1*y1 + (neg ? -1 : 1) * x2*y2 (radix 2^29 product

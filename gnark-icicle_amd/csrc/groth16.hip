@@ -162,6 +162,7 @@ int pk_upload_ranges(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsigned f
   pk->zlo = rg.loZ;
   pk->nbZ = rg.hiZ - rg.loZ;
   pk->precomp = (flags & GM_PK_PRECOMPUTE) != 0;
+  const bool precomp_auto = !pk->precomp && (flags & GM_PK_PRECOMPUTE_AUTO);
   const int frbits = curve == GM_BN254 ? CurveBN254::FR_BITS : CurveBLS12377::FR_BITS;
   auto fail = [&](int code) {
     pk_release(pk);
@@ -218,6 +219,29 @@ int pk_upload_ranges(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsigned f
     wire_plan_choice(span, pk->nbA, pk->nbB, pk->nbK, pk->wshare);
     wire_plan_maps(span, idx, cnt, pk->wshare, wmap);
   }
+  // GM_PK_PRECOMPUTE_AUTO: the window copies when they fit the device (the
+  // final arrays plus the largest array's transient upload buffers within
+  // GM_PK_PRECOMPUTE_FRAC of the free memory)
+  if (precomp_auto) {
+    const MsmPrecomp pw = msm_choose_precomp(span, frbits);
+    auto bytes_of = [&](size_t cnt, bool shared, bool g2) {
+      const MsmPrecomp p = shared ? pw : msm_choose_precomp(cnt, frbits);
+      return (double)internal_point_bytes(curve, g2) * (double)p.W * (double)(shared ? span : cnt);
+    };
+    const double arr[5] = {bytes_of(pk->nbA, pk->wshare[0], false), bytes_of(pk->nbB, pk->wshare[1], false),
+                           bytes_of(pk->nbK, pk->wshare[2], false), bytes_of(pk->nbZ, false, false),
+                           bytes_of(pk->nbB, pk->wshare[1], true)};
+    double need = 0, largest = 0;
+    for (double b : arr) {
+      need += b;
+      largest = std::max(largest, b);
+    }
+    need += largest / 8;  // gnark-layout staging of the largest array
+    size_t fr = 0, tot = 0;
+    const char* fenv = getenv("GM_PK_PRECOMPUTE_FRAC");
+    const double frac = fenv ? atof(fenv) : 0.6;
+    pk->precomp = hipMemGetInfo(&fr, &tot) == hipSuccess && need <= frac * (double)fr;
+  }
   if (pk->precomp) {
     const MsmPrecomp pw = msm_choose_precomp(span, frbits);
     auto geom = [&](size_t cnt, bool shared) {
@@ -271,10 +295,51 @@ int pk_upload_ranges(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsigned f
     hipFree(tmp);
     return r;
   };
+  // Wire-indexed (shared-plan) array from host memory: the gnark-layout points
+  // are expanded to the wire span first (infinity = (0, 0) where a wire has no
+  // point), then converted / precomputed straight into the final array -- no
+  // precomputed compacted copy is ever materialised (peak = final + span gnark
+  // points, not twice the final size).
+  auto up_expanded_gnark = [&](const void* hsrc, size_t count, bool g2, const MsmPrecomp& pre, void** dst,
+                               const std::vector<uint32_t>& emap) -> int {
+    const size_t gpb = g2 ? g2b : g1b;
+    void *tmp = nullptr, *wide = nullptr, *dmap = nullptr;
+    auto done = [&](int r) {
+      for (void* q : {tmp, wide, dmap})
+        if (q) hipFree(q);
+      return r;
+    };
+    int r = up(hsrc, gpb * count, &tmp);
+    if (r) return done(r);
+    if ((r = up(emap.data(), 4 * span, &dmap))) return done(r);
+    if (hipMalloc(&wide, gpb * (span ? span : 1)) != hipSuccess) {
+      set_error("pk upload: hipMalloc of an expanded array failed");
+      return done(GM_ERR_OOM);
+    }
+    const size_t q = gpb / 16, total = span * q;
+    if (span)
+      hipLaunchKernelGGL(k_expand_points, dim3(blocks_for(total, 256)), dim3(256), 0, ctx->stream, (const uint4*)tmp,
+                         count, (const uint32_t*)dmap, span, total, (uint32_t)q, (uint4*)wide);
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(ctx->stream) != hipSuccess) {
+      set_error("pk upload: expanding a point array failed");
+      return done(GM_ERR_DEVICE);
+    }
+    hipFree(tmp);
+    tmp = nullptr;
+    const size_t copies = pk->precomp ? pre.W : 1;
+    if (hipMalloc(dst, internal_point_bytes(curve, g2) * (span ? span * copies : 1)) != hipSuccess) {
+      set_error("pk upload hipMalloc: out of device memory");
+      return done(GM_ERR_OOM);
+    }
+    r = prepare_points_into(ctx, curve, g2, wide, span, pk->precomp ? &pre : nullptr, *dst);
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess && !r) r = GM_ERR_DEVICE;
+    return done(r);
+  };
   auto up_pts = [&](int which, const void* hsrc, size_t count, bool g2, const MsmPrecomp& pre, void** dst,
                     const std::vector<uint32_t>* emap) -> int {
     if (!emap) return up_compact(which, hsrc, count, g2, pre, dst);
-    MsmPrecomp pc = pre;  // compacted first (stride = count), then expanded to the span
+    if (!src) return up_expanded_gnark(hsrc, count, g2, pre, dst, *emap);
+    MsmPrecomp pc = pre;  // streamed (dump): compacted first (stride = count), then expanded to the span
     pc.stride = count;
     void* tmp = nullptr;
     int r = up_compact(which, hsrc, count, g2, pc, &tmp);
@@ -985,7 +1050,7 @@ int gm_g16_pk_upload_ex(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsigne
 int gm_g16_pk_upload_shard(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsigned flags, int rank, int world,
                            gm_g16_pk** out) {
   if (int rc = check_curve_id(curve)) return rc;
-  if (flags & ~(unsigned)GM_PK_PRECOMPUTE) {
+  if (flags & ~(unsigned)(GM_PK_PRECOMPUTE | GM_PK_PRECOMPUTE_AUTO)) {
     set_error("pk upload: unknown flags");
     return GM_ERR_INVALID;
   }
@@ -1003,6 +1068,12 @@ int gm_g16_pk_upload_shard(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsi
   shard_of(h->domain_size - 1, rank, world, &rg.loZ, &rg.hiZ);
   rg.rebase = false;
   return pk_upload_ranges(ctx, curve, h, flags, rg, out, nullptr);
+}
+
+int gm_g16_pk_precomputed(const gm_g16_pk* pk, int* out) {
+  if (!pk || !out) return GM_ERR_INVALID;
+  *out = pk->precomp ? 1 : 0;
+  return GM_OK;
 }
 
 int gm_g16_pk_free(gm_ctx* ctx, gm_g16_pk* pk) {

@@ -60,10 +60,12 @@ inline uint32_t precomp_narrow(uint32_t c, uint32_t W, int bits) {
 // `bits`-bit scalar field: minimises n*W accumulation adds + ~3 adds per bucket.
 MsmPrecomp msm_choose_precomp(size_t n, int bits);
 
-// Entry value whose point is skipped (treated as infinity, nothing loaded): a
-// plan shared by several point arrays maps the entries of points an array does
-// not have to it (groth16.hip, the shared wire plan).  Valid point indices stay
-// below 2^31 - 1 (msm_plan bounds n and W * stride by 2^31).
+// Host wire-map sentinel "this wire has no point" (groth16.hip, the shared wire
+// plan): k_expand_points writes an all-zero (infinity) point into the expanded
+// array's slot for such a wire.  It is never an entry value of a plan -- the
+// accumulation kernels have no skip branch, so an entry carrying it would fail
+// the bounds check (err = 2).  Valid point indices stay below 2^31 - 1
+// (msm_plan bounds n and W * stride by 2^31).
 constexpr uint32_t MSM_SKIP = 0x7fffffffu;
 
 // Sorted signed-digit plan of one scalar vector: depends only on the scalars

@@ -283,6 +283,12 @@ __global__ void __launch_bounds__(TPB) k_ntt_pass(Fe<P>* __restrict__ data, int 
 // (Harvey) round inputs < 4p, outputs < 4p.  Intermediate DIT passes store
 // lazily reduced (< 4p < 2^256; the next pass multiplies on load).
 // ---------------------------------------------------------------------------
+// waves per SIMD the radix-4 pass is compiled for (1: the compiler's choice);
+// A/B builds override it with -DNTT_R4_WPE=4
+#ifndef NTT_R4_WPE
+#define NTT_R4_WPE 1
+#endif
+
 // f(0), f(1), f(2), f(3) with compile-time indices (register-resident arrays)
 template <class F>
 GM_DEV void unroll4(F&& f) {
@@ -297,43 +303,45 @@ GM_DEV Fe<P> ntt_tw(const Fe<P>* __restrict__ sub, int i) {
   return sub[i];
 }
 
+// products of a round: one mad chain each (CH) or the compiler's split columns
+#define MUL(x, y) (CH ? fe_mul_lz_chain(x, y) : fe_mul_lz(x, y))
 // DIF radix-2 butterfly pair of one round: (u, v) -> (u + v, (u - v + Kp) w)
-template <class P>
+template <class P, bool CH>
 GM_DEV void r4_dif(Fe<P> (&e)[4], const Fe<P>& t1, const Fe<P>& t2, const Fe<P>& t3) {
   // stage lm: (e0, e2) by w_2m^jj, (e1, e3) by w_2m^(jj+s); inputs < 2p
   const Fe<P> s0 = fe_add_lz(e[0], e[2]);                        // < 4p
-  const Fe<P> d0 = fe_mul_lz(fe_sub_lz<2>(e[0], e[2]), t1);      // < 2p
+  const Fe<P> d0 = MUL(fe_sub_lz<2>(e[0], e[2]), t1);      // < 2p
   const Fe<P> s1 = fe_add_lz(e[1], e[3]);                        // < 4p
-  const Fe<P> d1 = fe_mul_lz(fe_sub_lz<2>(e[1], e[3]), t2);      // < 2p
+  const Fe<P> d1 = MUL(fe_sub_lz<2>(e[1], e[3]), t2);      // < 2p
   // stage lm - 1: (s0, s1), (d0, d1) by w_m^jj
   e[0] = fe_add_lz(s0, s1);                                      // < 8p
   fe_reduce_k<4>(e[0]);
   fe_reduce_k<2>(e[0]);                                          // < 2p
-  e[1] = fe_mul_lz(fe_sub_lz<4>(s0, s1), t3);                    // < 2p
+  e[1] = MUL(fe_sub_lz<4>(s0, s1), t3);                    // < 2p
   e[2] = fe_add_lz(d0, d1);                                      // < 4p
   fe_reduce_k<2>(e[2]);                                          // < 2p
-  e[3] = fe_mul_lz(fe_sub_lz<2>(d0, d1), t3);                    // < 2p
+  e[3] = MUL(fe_sub_lz<2>(d0, d1), t3);                    // < 2p
 }
 // the s = 1 DIF round (twiddles 1, w_4, 1): inputs < 2p, outputs < 8p
-template <class P>
+template <class P, bool CH>
 GM_DEV void r4_dif_w4(Fe<P> (&e)[4], const Fe<P>& w4) {
   const Fe<P> s0 = fe_add_lz(e[0], e[2]);                        // < 4p
   const Fe<P> d0 = fe_sub_lz<2>(e[0], e[2]);                     // < 4p
   const Fe<P> s1 = fe_add_lz(e[1], e[3]);                        // < 4p
-  const Fe<P> d1 = fe_mul_lz(fe_sub_lz<2>(e[1], e[3]), w4);      // < 2p
+  const Fe<P> d1 = MUL(fe_sub_lz<2>(e[1], e[3]), w4);      // < 2p
   e[0] = fe_add_lz(s0, s1);                                      // < 8p
   e[1] = fe_sub_lz<4>(s0, s1);                                   // < 8p
   e[2] = fe_add_lz(d0, d1);                                      // < 6p
   e[3] = fe_sub_lz<2>(d0, d1);                                   // < 6p
 }
 // DIT (Harvey) round: (u, v) -> (u + v w, u - v w + 2p); inputs < 4p, outputs < 4p
-template <class P>
+template <class P, bool CH>
 GM_DEV void r4_dit(Fe<P> (&e)[4], const Fe<P>& a, const Fe<P>& b, const Fe<P>& c) {
   // stage lm: (e0, e1), (e2, e3) by w_2m^jj
   fe_reduce_k<2>(e[0]);
   fe_reduce_k<2>(e[2]);
-  const Fe<P> v1 = fe_mul_lz(e[1], a);                           // < 2p
-  const Fe<P> v3 = fe_mul_lz(e[3], a);
+  const Fe<P> v1 = MUL(e[1], a);                           // < 2p
+  const Fe<P> v3 = MUL(e[3], a);
   Fe<P> s0 = fe_add_lz(e[0], v1);                                // < 4p
   Fe<P> s1 = fe_sub_lz<2>(e[0], v1);
   const Fe<P> s2 = fe_add_lz(e[2], v3);
@@ -341,20 +349,20 @@ GM_DEV void r4_dit(Fe<P> (&e)[4], const Fe<P>& a, const Fe<P>& b, const Fe<P>& c
   // stage lm + 1: (s0, s2) by w_4m^jj, (s1, s3) by w_4m^(jj+s)
   fe_reduce_k<2>(s0);
   fe_reduce_k<2>(s1);
-  const Fe<P> x = fe_mul_lz(s2, b);
-  const Fe<P> y = fe_mul_lz(s3, c);
+  const Fe<P> x = MUL(s2, b);
+  const Fe<P> y = MUL(s3, c);
   e[0] = fe_add_lz(s0, x);
   e[2] = fe_sub_lz<2>(s0, x);
   e[1] = fe_add_lz(s1, y);
   e[3] = fe_sub_lz<2>(s1, y);
 }
 // the s = 1 DIT round (twiddles 1, 1, w_4): inputs < 2p, outputs < 4p
-template <class P>
+template <class P, bool CH>
 GM_DEV void r4_dit_w4(Fe<P> (&e)[4], const Fe<P>& w4) {
   const Fe<P> s0 = fe_add_lz(e[0], e[1]);                        // < 4p
   const Fe<P> s1 = fe_sub_lz<2>(e[0], e[1]);                     // < 4p
   const Fe<P> s2 = fe_add_lz(e[2], e[3]);                        // < 4p
-  const Fe<P> y = fe_mul_lz(fe_sub_lz<2>(e[2], e[3]), w4);       // < 2p
+  const Fe<P> y = MUL(fe_sub_lz<2>(e[2], e[3]), w4);       // < 2p
   e[0] = fe_add_lz(s0, s2);                                      // < 8p
   e[2] = fe_sub_lz<4>(s0, s2);                                   // < 8p
   e[1] = fe_add_lz(s1, y);                                       // < 6p
@@ -362,8 +370,10 @@ GM_DEV void r4_dit_w4(Fe<P> (&e)[4], const Fe<P>& w4) {
   unroll4([&](auto I) { fe_reduce_k<4>(e[I]); });               // < 4p
 }
 
-template <class P, bool DIT>
-__global__ void __launch_bounds__(NTT_TPB) k_ntt_pass4(Fe<P>* __restrict__ data, int logn, int lo, int t,
+#undef MUL
+
+template <class P, bool DIT, bool CH = false>
+__global__ void __launch_bounds__(NTT_TPB) __attribute__((amdgpu_waves_per_eu(NTT_R4_WPE))) k_ntt_pass4(Fe<P>* __restrict__ data, int logn, int lo, int t,
                                                        const Fe<P>* __restrict__ tw,
                                                        const Fe<P>* __restrict__ sub,
                                                        const Fe<P>* __restrict__ pre,
@@ -417,12 +427,12 @@ __global__ void __launch_bounds__(NTT_TPB) k_ntt_pass4(Fe<P>* __restrict__ data,
     const int jj = k & (s - 1);
     if (s == 1) {  // block-uniform
       const Fe<P> w4 = ntt_tw(sub, 1 << (t - 2));
-      if (DIT) r4_dit_w4(e, w4);
-      else r4_dif_w4(e, w4);
+      if (DIT) r4_dit_w4<P, CH>(e, w4);
+      else r4_dif_w4<P, CH>(e, w4);
     } else if (!DIT) {
-      r4_dif(e, ntt_tw(sub, jj << (t - ls - 2)), ntt_tw(sub, (jj + s) << (t - ls - 2)), ntt_tw(sub, jj << (t - ls - 1)));
+      r4_dif<P, CH>(e, ntt_tw(sub, jj << (t - ls - 2)), ntt_tw(sub, (jj + s) << (t - ls - 2)), ntt_tw(sub, jj << (t - ls - 1)));
     } else {
-      r4_dit(e, ntt_tw(sub, jj << (t - ls - 1)), ntt_tw(sub, jj << (t - ls - 2)), ntt_tw(sub, (jj + s) << (t - ls - 2)));
+      r4_dit<P, CH>(e, ntt_tw(sub, jj << (t - ls - 1)), ntt_tw(sub, jj << (t - ls - 2)), ntt_tw(sub, (jj + s) << (t - ls - 2)));
     }
   }
   if (t & 1) {
@@ -798,6 +808,8 @@ static int run_passes(gm_ctx* ctx, NttDomain<C>* d, Fe<typename C::Fr>* a, bool 
   static const bool swg = getenv("GM_NTT_SWG") ? atoi(getenv("GM_NTT_SWG")) != 0 : true;
   // radix-4 passes (k_ntt_pass4) by default; GM_NTT_R4=0: the radix-2 kernel (A/B)
   static const bool r4 = getenv("GM_NTT_R4") ? atoi(getenv("GM_NTT_R4")) != 0 : true;
+  // GM_NTT_CHAIN=1: one dependent mad chain per product (fe_mul CHAIN; A/B)
+  static const bool r4chain = getenv("GM_NTT_CHAIN") ? atoi(getenv("GM_NTT_CHAIN")) != 0 : false;
   const size_t smem = sizeof(Fe<Fr>) * (NTT_TILE + (swg ? 0 : (1 << (NTT_TMAX - 1))));
   const int np = (int)d->passes.size();
   for (int k = 0; k < np; k++) {
@@ -812,7 +824,8 @@ static int run_passes(gm_ctx* ctx, NttDomain<C>* d, Fe<typename C::Fr>* a, bool 
     const unsigned grid = (unsigned)((nother + B - 1) / B);
     ProfScope pscope(ctx, "ntt_pass");
     if (r4 && ps.t >= 2) {
-      auto k4 = dit ? k_ntt_pass4<Fr, true> : k_ntt_pass4<Fr, false>;
+      auto k4 = dit ? (r4chain ? k_ntt_pass4<Fr, true, true> : k_ntt_pass4<Fr, true>)
+                    : (r4chain ? k_ntt_pass4<Fr, false, true> : k_ntt_pass4<Fr, false>);
       hipLaunchKernelGGL(k4, dim3(grid), dim3(NTT_TPB),
                          sizeof(Fe<Fr>) * NTT_TILE, st, a, d->logn, ps.lo, ps.t, tw, sub, first ? fz.pre : nullptr,
                          last ? fz.post : nullptr, first ? fz.pb : nullptr, first ? fz.pc : nullptr);

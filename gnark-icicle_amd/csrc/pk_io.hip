@@ -268,7 +268,7 @@ int gm_g16_pk_upload_dump_shard(gm_ctx* ctx, int curve, const gm_g16_pk_host* me
                                 unsigned flags, int rank, int world, uint64_t* end_offset, gm_g16_pk** out) {
   if (int rc = check_curve_id(curve)) return rc;
   if (!ctx || !meta || !out || fd < 0 || meta->domain_size < 2) return GM_ERR_INVALID;
-  if (flags & ~(unsigned)GM_PK_PRECOMPUTE) {
+  if (flags & ~(unsigned)(GM_PK_PRECOMPUTE | GM_PK_PRECOMPUTE_AUTO)) {
     set_error("pk dump: unknown flags");
     return GM_ERR_INVALID;
   }
@@ -413,13 +413,19 @@ int gm_g16_pk_load_cache(gm_ctx* ctx, int fd, gm_g16_pk** out) {
   }
   for (int x = 0; x < 3; x++) pk->wshare[x] = (h.wshare >> x) & 1;
   if (pk->precomp && h.wshare) {
-    pk->preW = msm_choose_precomp(pk->whi - pk->wlo, frbits);
-    pk->preW.stride = pk->whi - pk->wlo;
+    // the wire plan's window geometry is the one the wire-indexed arrays were
+    // built with (their header fields), not a re-derivation by this build's
+    // window cost model: a cache stays loadable when the chooser changes.  The
+    // shared arrays must agree with each other and span the wire slice.
     const MsmPrecomp* shared[3] = {&pk->preA, &pk->preB, &pk->preK};
+    int first = -1;
+    for (int x = 0; x < 3; x++)
+      if (pk->wshare[x] && first < 0) first = x;
+    pk->preW = *shared[first];
     for (int x = 0; x < 3; x++)
       if (pk->wshare[x] && (shared[x]->c != pk->preW.c || shared[x]->W != pk->preW.W ||
-                            shared[x]->narrow != pk->preW.narrow || shared[x]->stride != pk->preW.stride)) {
-        set_error("pk cache: wire-indexed array without the wire plan's window geometry");
+                            shared[x]->narrow != pk->preW.narrow || shared[x]->stride != pk->whi - pk->wlo)) {
+        set_error("pk cache: wire-indexed arrays with different window geometries");
         return fail(GM_ERR_INVALID);
       }
   }

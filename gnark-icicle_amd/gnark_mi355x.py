@@ -46,7 +46,7 @@ SYMBOLS = [
     "gm_msm_precomputed", "gm_kzg_commit", "gm_ntt",
     "gm_poly_ops", "gm_reverse_scalars", "gm_groth16_compute_h", "gm_g16_pk_upload", "gm_g16_pk_upload_ex", "gm_g16_pk_upload_shard",
     "gm_g16_partial_bytes", "gm_g16_prove_partial", "gm_g16_finish",
-    "gm_g16_pk_free", "gm_g16_prove", "gm_g16_prove_device", "gm_jac_add", "gm_jac_to_affine",
+    "gm_g16_pk_free", "gm_g16_pk_precomputed", "gm_g16_prove", "gm_g16_prove_device", "gm_jac_add", "gm_jac_to_affine",
     "gm_batch_mul_base", "gm_random_scalars", "gm_generator", "gm_test_field_op",
     "gm_test_point_op", "gm_icicle_generate_twiddles", "gm_icicle_intt_on_device", "gm_icicle_ntt_on_device",
     "gm_icicle_poly_ops", "gm_device_count", "gm_multi_init", "gm_multi_destroy", "gm_multi_size",
@@ -111,6 +111,7 @@ def load_library(path: str = LIB_PATH):
     L.gm_g16_prove_partial.argtypes = [vp, vp, vp, vp, vp, vp, sz, vp]
     L.gm_g16_finish.argtypes = [i, vp, vp, vp, vp, vp, vp, vp]
     L.gm_g16_pk_free.argtypes = [vp, vp]
+    L.gm_g16_pk_precomputed.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
     L.gm_g16_prove.argtypes = [vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, vp, vp]
     L.gm_g16_prove_device.argtypes = [vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, vp, vp]
     L.gm_r1cs_upload.argtypes = [vp, i, sz, sz, vp, vp, vp, vp, sz, vp]
@@ -588,6 +589,21 @@ class ProvingKey:
     """
 
     PRECOMPUTE = 1  # GM_PK_PRECOMPUTE
+    PRECOMPUTE_AUTO = 2  # GM_PK_PRECOMPUTE_AUTO: window copies iff they fit the device
+
+    @classmethod
+    def _flags(cls, precompute):
+        """precompute: False / True / "auto" (GM_PK_PRECOMPUTE_AUTO)."""
+        if precompute == "auto":
+            return cls.PRECOMPUTE_AUTO
+        return cls.PRECOMPUTE if precompute else 0
+
+    @property
+    def precomputed(self) -> bool:
+        """Whether the device key holds the window copies (the auto choice)."""
+        v = ctypes.c_int()
+        _check(load_library().gm_g16_pk_precomputed(self.handle, ctypes.byref(v)))
+        return bool(v.value)
 
     def __init__(self, ctx: Context, curve, pk: dict, domain_size: int, nb_wires: int, nb_public: int,
                  precompute: bool = False, shard=None, pk_is_shard: bool = False):
@@ -597,7 +613,7 @@ class ProvingKey:
         self._keep = arrs
         self._h = h
         handle = ctypes.c_void_p()
-        flags = self.PRECOMPUTE if precompute else 0
+        flags = self._flags(precompute)
         rank, world = shard if shard is not None else (0, 1)
         _check(load_library().gm_g16_pk_upload_shard(ctx.handle, self.curve, ctypes.byref(h), flags, rank, world,
                                                      ctypes.byref(handle)))
@@ -631,7 +647,7 @@ class ProvingKey:
         fd = os.open(path, os.O_RDONLY)
         try:
             _check(load_library().gm_g16_pk_upload_dump_shard(ctx.handle, self.curve, ctypes.byref(h),
-                                                              fd, offset, self.PRECOMPUTE if precompute else 0,
+                                                              fd, offset, cls._flags(precompute),
                                                               rank, world, ctypes.byref(end), ctypes.byref(handle)))
         finally:
             os.close(fd)

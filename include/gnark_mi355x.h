@@ -224,6 +224,14 @@ int gm_g16_pk_upload(gm_ctx* ctx, int curve, const gm_g16_pk_host* pk, gm_g16_pk
  * ~77 GB for a BN254 2^24 key) -- fewer windows and one bucket reduction per
  * MSM.  gm_g16_pk_upload(...) == gm_g16_pk_upload_ex(..., 0, ...). */
 #define GM_PK_PRECOMPUTE 1u
+/* GM_PK_PRECOMPUTE_AUTO: precompute when the window copies fit the device --
+ * the key's precomputed arrays plus the upload's transient buffers take at
+ * most GM_PK_PRECOMPUTE_FRAC (default 0.6) of the free device memory at upload
+ * time (hipMemGetInfo); otherwise a plain key.  On a 288 GB MI355X a BN254
+ * 2^24 key (~77 GB precomputed) qualifies.  gm_g16_pk_precomputed() reports
+ * the choice. */
+#define GM_PK_PRECOMPUTE_AUTO 2u
+int gm_g16_pk_precomputed(const gm_g16_pk* pk, int* out);
 int gm_g16_pk_upload_ex(gm_ctx* ctx, int curve, const gm_g16_pk_host* pk, unsigned flags, gm_g16_pk** out);
 int gm_g16_pk_free(gm_ctx* ctx, gm_g16_pk* pk);
 

@@ -44,6 +44,24 @@ const (
 // on the device(s) (GM_PK_PRECOMPUTE).
 const PkPrecompute = C.GM_PK_PRECOMPUTE
 
+// PkPrecomputeAuto takes the window copies only when they fit the device
+// (GM_PK_PRECOMPUTE_AUTO: at most 60% of the free HBM at upload; a BN254 2^24
+// key needs ~77 GB of an MI355X's 288 GB).
+const PkPrecomputeAuto = C.GM_PK_PRECOMPUTE_AUTO
+
+// PrecomputeFlags maps GNARK_MI355X_PRECOMPUTE to upload flags: "1" always,
+// "0" never, unset or "auto" when the copies fit (PkPrecomputeAuto).
+func PrecomputeFlags() uint {
+	switch os.Getenv("GNARK_MI355X_PRECOMPUTE") {
+	case "1":
+		return PkPrecompute
+	case "0":
+		return 0
+	default:
+		return PkPrecomputeAuto
+	}
+}
+
 func lastErr(what string, rc C.int) error {
 	return fmt.Errorf("gnark_mi355x %s: status %d: %s", what, int(rc), C.GoString(C.gm_last_error()))
 }

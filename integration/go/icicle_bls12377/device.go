@@ -6,11 +6,7 @@
 // NOT COMPILED HERE: this image has no Go toolchain.
 package icicle_bls12377
 
-import (
-	"os"
-
-	"github.com/consensys/gnark/backend/accel/mi355x/gm"
-)
+import "github.com/consensys/gnark/backend/accel/mi355x/gm"
 
 type deviceInfo struct {
 	key *gm.G16Key
@@ -25,4 +21,3 @@ func (pk *ProvingKey) FreeDevice() {
 	}
 }
 
-func precomputeRequested() bool { return os.Getenv("GNARK_MI355X_PRECOMPUTE") == "1" }

@@ -67,8 +67,9 @@ func kWires(r1cs *cs.R1CS, nbWires int) []uint32 {
 }
 
 // setupDevicePointers uploads the key once (icicle.go:31-130).  The point arrays
-// are converted to the MSM layout on the device; GNARK_MI355X_PRECOMPUTE=1 also
-// keeps fixed-base window copies (~12x the point memory, -20% prove time at 2^24).
+// are converted to the MSM layout on the device; by default the key also keeps
+// fixed-base window copies when they fit the device (~12x the point memory,
+// -14% prove time at 2^24; GNARK_MI355X_PRECOMPUTE=0 / 1 forces them off / on).
 func (pk *ProvingKey) setupDevicePointers(r1cs *cs.R1CS) error {
 	if pk.deviceInfo != nil {
 		return nil
@@ -95,10 +96,7 @@ func (pk *ProvingKey) setupDevicePointers(r1cs *cs.R1CS) error {
 	if len(pk.G2.B) > 0 {
 		k.B2 = unsafe.Pointer(&pk.G2.B[0])
 	}
-	flags := uint(0)
-	if precomputeRequested() {
-		flags |= gm.PkPrecompute
-	}
+	flags := gm.PrecomputeFlags() // default: window copies when they fit the device
 	key, err := gm.UploadG16Key(gm.BLS12_377, k, flags)
 	if err != nil {
 		return err

@@ -39,7 +39,6 @@ func (pk *ProvingKey) FreeDevice() {
 	}
 }
 
-func precomputeRequested() bool { return os.Getenv("GNARK_MI355X_PRECOMPUTE") == "1" }
 
 // ReadDumpToDevice reads a key written by groth16_bn254.ProvingKey.WriteDump
 // (backend/groth16/bn254/marshal.go:389-456) like ReadDump (:460-550) does,
@@ -89,10 +88,7 @@ func (pk *ProvingKey) ReadDumpToDevice(f *os.File, r1cs *cs.R1CS) error {
 		Beta2: goUnsafe.Pointer(&pk.G2.Beta), Delta2: goUnsafe.Pointer(&pk.G2.Delta),
 		InfA:  pk.InfinityA, InfB: pk.InfinityB, KWires: kw,
 	}
-	flags := uint(0)
-	if precomputeRequested() {
-		flags |= gm.PkPrecompute
-	}
+	flags := gm.PrecomputeFlags()
 	key, end, err := gm.UploadG16KeyDump(gm.BN254, k, f, cr.n, flags)
 	if err != nil {
 		return err

@@ -389,3 +389,26 @@ def test_install_into_a_reference_checkout(tmp_path):
                 s = (g / rel / f).read_text()
                 if eval_build(build_expr(s), frozenset()):
                     assert "C" not in imports(s) and not any(i.endswith("/mi355x/gm") for i in imports(s)), (rel, f)
+
+
+def test_every_import_is_used():
+    """Go refuses unused imports; without a Go toolchain here, check that each
+    imported package's name (alias or last path element) is referenced."""
+    bad = []
+    for p in go_files():
+        src = open(p).read()
+        code = strip_go(src)
+        specs = re.findall(r'(?m)^import\s+(\w+\s+)?"([^"]+)"', src)
+        for block in re.findall(r"(?ms)^import \((.*?)^\)", src):
+            specs += re.findall(r'(?m)^\s*(\w+\s+|_\s+|\.\s+)?"([^"]+)"', block)
+        for alias, path in specs:
+            alias = alias.strip()
+            if path == "C" or alias in ("_", "."):
+                continue
+            name = alias or path.rstrip("/").split("/")[-1]
+            if name.startswith("v") and name[1:].isdigit():  # major-version suffix
+                name = path.split("/")[-2]
+            name = name.replace("-", "")
+            if not re.search(r"\b" + re.escape(name) + r"\.", code):
+                bad.append(f"{os.path.relpath(p, ROOT)}: import {path!r} ({name}) unused")
+    assert not bad, "\n".join(bad)

@@ -269,3 +269,29 @@ def test_groth16_shared_wire_plan_on_off(gm_ctx, oracle, monkeypatch, precompute
             assert dpk.prove(enc(W), enc(a), enc(b), enc(cc), rb, sb) == exp, flag
         finally:
             dpk.free()
+
+
+@pytest.mark.parametrize("frac,expect", [("0.6", True), ("0.000000001", False)])
+def test_groth16_precompute_auto(gm_ctx, oracle, monkeypatch, frac, expect):
+    """GM_PK_PRECOMPUTE_AUTO (the Go hook's default): the key takes the window
+    copies when they fit GM_PK_PRECOMPUTE_FRAC of the free device memory, else
+    stays plain; either way the proof is the oracle's.  The shared wire plan's
+    arrays are expanded in gnark layout before the precomputation (no
+    compacted precomputed copy), which this key exercises (3 dropped A wires)."""
+    import gnark_mi355x as gm
+    cname = "bn254"
+    c = pyref.CURVES[cname]
+    r1, W = R.squaring_chain(2000, cname, x=7)
+    tox = R.encode_vec(cname, [t % c.r for t in TOXIC])
+    pk = oracle.g16_setup(cname, r1, tox)
+    a, b, cc = r1.solve_abc(W)
+    enc = lambda v: R.encode_vec(cname, v)
+    rb, sb = enc([0x5151]), enc([0x7373])
+    exp = oracle.g16_prove(cname, pk, r1.nb_public, enc(W), enc(a), enc(b), enc(cc), rb, sb)
+    monkeypatch.setenv("GM_PK_PRECOMPUTE_FRAC", frac)
+    dpk = gm.ProvingKey(gm_ctx, cname, pk, r1.domain_size, r1.nb_wires, r1.nb_public, precompute="auto")
+    try:
+        assert dpk.precomputed is expect
+        assert dpk.prove(enc(W), enc(a), enc(b), enc(cc), rb, sb) == exp
+    finally:
+        dpk.free()
