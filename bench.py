@@ -37,6 +37,14 @@ MADS_PER_MIXED_ADD = 6 * 162 + 2 * 126 + 243
 # profiles/r01_isa_rate.txt): 1024 SIMDs x 64 lanes x 2.4 GHz / 5.12 = 30.7 T/s
 MAD_PEAK_T = 1024 * 64 * 2.4e9 / 5.12 / 1e12
 NTT_BYTES_PER_ELEM = 64   # one 32 B read + one 32 B write per transform
+# algorithmic HBM bytes of one config-4 Groth16 prove per domain
+# element: 4 x 96 (G1 MSMs) + 160 (G2 MSM) + 7 x 64 (NTT / INTT) + 128 (PolyOps)
+G16_BYTES_PER_ELEM = 4 * 96 + 160 + 7 * 64 + 128
+# committed rocprofv3 --pmc summaries the roofline's traffic / valu fields are
+# read from (collected by tools/gpu_pmc.sh / tools/pmc_traffic.py on the bench's
+# own MSM workload; NOT measured inside this run)
+PMC_TRAFFIC_FILE = "profiles/r03h_pmc_traffic.json"
+PMC_VALU_FILE = "profiles/r03h_pmc_valu.json"
 
 
 def parse():
@@ -61,7 +69,7 @@ def parse():
 
 def load_pmc_traffic(name):
     """HBM bytes per launch from a committed rocprofv3 --pmc summary (or None)."""
-    p = os.path.join(ROOT, "profiles", "r03h_pmc_traffic.json")
+    p = os.path.join(ROOT, PMC_TRAFFIC_FILE)
     try:
         with open(p) as f:
             return json.load(f).get(name)
@@ -71,7 +79,7 @@ def load_pmc_traffic(name):
 
 def load_pmc_valu(name):
     """VALU utilisation of a kernel from the committed PMC summary (or None)."""
-    p = os.path.join(ROOT, "profiles", "r03h_pmc_valu.json")
+    p = os.path.join(ROOT, PMC_VALU_FILE)
     try:
         with open(p) as f:
             return json.load(f).get(name)
@@ -179,6 +187,8 @@ def main():
         "unit": "GB/s",
         "frac": round(achieved_gbs / HBM_PEAK_GBS, 5),
         "traffic": load_pmc_traffic("k_msm_accum_seg"),
+        "traffic_source": PMC_TRAFFIC_FILE + " (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this MSM "
+                          "workload, 2 x FETCH + WRITE per launch; committed profile, not measured in this run)",
         "avg_launch_ms": round(acc_avg_ms, 4),
         "bytes_per_launch": alg_bytes,
         "int_alu": {"achieved": round(tmads, 3), "peak": round(MAD_PEAK_T, 2), "unit": "T v_mad_u64_u32/s",
@@ -186,6 +196,7 @@ def main():
                     "work": "%d %spoints x %d windows XYZZ mixed adds x %d mads" % (
                         npts, "GLV (P, phi(P)) " if glv else "", windows, MADS_PER_MIXED_ADD)},
         "valu": load_pmc_valu("k_msm_accum_seg<Fe<Bn254Fp> >"),
+        "valu_source": PMC_VALU_FILE + " (rocprofv3 --pmc SQ_* passes; committed profile, not measured in this run)",
         "note": "bound=hbm is the bench contract's roofline for this non-MFMA path; the kernel is NOT HBM-bound: "
                 "its binding resource is VALU issue -- rocprofv3 PMC (profiles/r03h_pmc_valu.json) shows VALUBusy "
                 "~0.87 (gfx9 formula, 4 cycles/instr) for k_msm_accum_seg, ~2560 VALU instructions per mixed add; "
@@ -431,6 +442,7 @@ def groth16_bench(ctx, gm, logn, precompute=True, check_oracle=False):
     ch.free()
     med = lambda v: sorted(v)[len(v) // 2]
     res = {"logn": logn, "pk": "precomputed" if precompute else "plain",
+           "roofline": groth16_roofline(n, nb_wires, precompute, med(t_dev)),
            "prove_ms_host_inputs": round(med(t_host) * 1e3, 3), "prove_ms_device_inputs": round(med(t_dev) * 1e3, 3),
            "prove_ms_r1cs_resident": round(med(t_r1cs) * 1e3, 3),
            "best_ms": {"host_inputs": round(min(t_host) * 1e3, 3), "device_inputs": round(min(t_dev) * 1e3, 3),
@@ -472,6 +484,61 @@ def groth16_bench(ctx, gm, logn, precompute=True, check_oracle=False):
                       "prove.go:62-325, not gnark-crypto (no Go toolchain on the box)" % logn,
             "gpu_over_cpu": round(cpu_s * 1e3 / max(res["prove_ms_host_inputs"], 1e-9), 1)}
     return res
+
+
+def _choose_window(n, bits=254):
+    """msm_impl.hpp choose_window: c in [8, 20] minimising n W + 3 W 2^(c-1)."""
+    best = None
+    for c in range(8, 21):
+        W = -(-(bits + 1) // c)
+        cost = n * W + 3 * W * (1 << (c - 1))
+        if best is None or cost < best[0]:
+            best = (cost, c, W)
+    return best[1], best[2]
+
+
+def _choose_precomp(n, bits=254):
+    """msm_sort.hip msm_choose_precomp: c in [8, 24] minimising n W + 3 2^(c-1)."""
+    best = None
+    for c in range(8, 25):
+        W = -(-(bits + 1) // c)
+        cost = n * W + 3 * (1 << (c - 1))
+        if best is None or cost < best[0]:
+            best = (cost, c, W)
+    return best[1], best[2]
+
+
+# v_mad_u64_u32 per lazily reduced XYZZ mixed add (ISA counts of the
+# accumulation loops, tools/isa_blocks.py): BN254 G1 one lane; BN254 G2 both
+# lanes of a lane pair (pair_fp2.hpp, four-product Y3)
+MADS_G1_ADD = MADS_PER_MIXED_ADD
+MADS_G2_ADD = 2 * 1701  # per lane: 1296 + 405 in the k_msm_accum_seg_pair loop blocks
+
+
+def groth16_roofline(n, nb_wires, precompute, t_s):
+    """Roofline of one Groth16 prove at n = 2^logn (device inputs, the kernels'
+    own time scope): SURVEY §8d's algorithmic bytes (1120 B per domain element)
+    over the prove time against HBM, and the summed MSM bucket-add mads over the
+    prove time against the measured mad-only peak (int_alu)."""
+    choose = _choose_precomp if precompute else _choose_window
+    _, W = choose(nb_wires)      # A, B, B2, K: the shared wire plan over the wires
+    _, Wz = choose(n - 1)        # Z over h[:n-1]
+    g1_adds = 3 * nb_wires * W + (n - 1) * Wz
+    g2_adds = nb_wires * W
+    mads = g1_adds * MADS_G1_ADD + g2_adds * MADS_G2_ADD
+    nbytes = G16_BYTES_PER_ELEM * n
+    gbs = nbytes / t_s / 1e9
+    tm = mads / t_s / 1e12
+    return {"bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(gbs / HBM_PEAK_GBS, 5), "bytes_per_prove": nbytes, "traffic": None,
+            "basis": "SURVEY.md 8d: 4 x 96 n (G1 MSMs) + 160 n (G2 MSM) + 7 x 64 n (NTTs) + 128 n (PolyOps) "
+                     "over prove_ms_device_inputs",
+            "int_alu": {"achieved": round(tm, 3), "peak": round(MAD_PEAK_T, 2), "unit": "T v_mad_u64_u32/s",
+                        "frac": round(tm / MAD_PEAK_T, 4),
+                        "work": "%d G1 + %d G2 mixed adds (W = %d, Wz = %d windows%s) x %d / %d mads; NTTs and "
+                                "reductions not counted" % (g1_adds, g2_adds, W, Wz,
+                                                             ", precomputed" if precompute else "",
+                                                             MADS_G1_ADD, MADS_G2_ADD)}}
 
 
 def staged_and_io_bench(ctx, gm, dpk, pk, n, nb_wires, nb_public, host, r, host_proof):

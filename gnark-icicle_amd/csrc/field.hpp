@@ -417,6 +417,41 @@ GM_DEV Fe<P> fe_mul2_redc(const Fe<P>& x1, const Fe<P>& y1, const Fe<P>& x2, con
   return r;
 }
 
+// Unsigned Montgomery reduction of x1*y1 + x2*y2 (radix 2^29 product scanning,
+// one 64-bit column accumulator, no per-lane sign): the lane-pair Fp2 product
+// negates its second operand up front (fe_negk_cf) instead of subtracting the
+// product, so both lanes of a pair run the same instructions.  Column bound:
+// N (2^58 + 2^59 + 2^58) < 2^64 for N <= 14 with x1, y1, y2 normalised and x2
+// limbs < 2^30.  Output < (x1 y1 + x2 y2) / R' + p, limbs normalised.
+template <class P>
+GM_DEV Fe<P> fe_mul2_redc_u(const Fe<P>& x1, const Fe<P>& y1, const Fe<P>& x2, const Fe<P>& y2) {
+  constexpr int N = P::N;
+  static_assert(N <= 14, "unsigned two-product column bound");
+  uint32_t m[N];
+  Fe<P> r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * N - 1; k++) {
+#pragma unroll
+    for (int i = (k - N + 1 > 0 ? k - N + 1 : 0); i <= (k < N - 1 ? k : N - 1); i++) {
+      acc += (uint64_t)x1.v[i] * y1.v[k - i];
+      acc += (uint64_t)x2.v[i] * y2.v[k - i];
+    }
+#pragma unroll
+    for (int i = (k - N + 1 > 0 ? k - N + 1 : 0); i <= (k - 1 < N - 1 ? k - 1 : N - 1); i++)
+      acc += (uint64_t)m[i] * P::p(k - i);
+    if (k < N) {
+      m[k] = ((uint32_t)acc * P::INV) & LIMB_MASK;
+      acc += (uint64_t)m[k] * P::p(0);
+    } else {
+      r.v[k - N] = (uint32_t)acc & LIMB_MASK;
+    }
+    acc >>= RADIX;
+  }
+  r.v[N - 1] = (uint32_t)acc;
+  return r;
+}
+
 // a + b, no reduction (limbs normalised)
 template <class P>
 GM_DEV Fe<P> fe_add_lz(const Fe<P>& a, const Fe<P>& b) {
@@ -465,6 +500,24 @@ template <class P>
 GM_HD constexpr uint32_t p2_borrowed_limb(int i) {
   return i == 0 ? kp_limb<P, 2>(0) + (1u << RADIX)
                 : (i == P::N - 1 ? kp_limb<P, 2>(i) - 1u : kp_limb<P, 2>(i) + (1u << RADIX) - 1u);
+}
+// Limb i of K p in borrowed form (as p2_borrowed_limb): every limb below the
+// top is >= 2^29 - 1, so K p - s needs no carries for normalised s.
+template <class P, int K>
+GM_HD constexpr uint32_t kp_borrowed_limb(int i) {
+  return i == 0 ? kp_limb<P, K>(0) + (1u << RADIX)
+                : (i == P::N - 1 ? kp_limb<P, K>(i) - 1u : kp_limb<P, K>(i) + (1u << RADIX) - 1u);
+}
+// K p - s for s < (K - 1) p with normalised limbs, carry-free (one VOP2 per
+// limb): limbs < 2^30, the top limb non-negative (s's top limb is at least p's
+// top limb below K p's).  A product operand (fe_mul2_redc_u's x2), not a
+// canonical value.
+template <int K, class P>
+GM_DEV Fe<P> fe_negk_cf(const Fe<P>& s) {
+  Fe<P> r;
+#pragma unroll
+  for (int i = 0; i < P::N; i++) r.v[i] = kp_borrowed_limb<P, K>(i) - s.v[i];
+  return r;
 }
 // neg ? 2p - s : s for s < 2p with normalised limbs, carry-free (2 VOP2 per limb
 // instead of a borrow chain plus a masked add of p).  The limbs of 2p - s are left

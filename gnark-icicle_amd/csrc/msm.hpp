@@ -114,6 +114,7 @@ int msm_run(gm_ctx* ctx, const MsmPlan& plan, const void* points_internal,
 struct MsmTail {
   size_t n = 0, M = 0;
   uint32_t c = 0, W = 0, Wr = 0, nb = 0, total = 0, L = 0, nseg = 0, K = 0, Q = 2;
+  uint32_t wn = 0;  // first narrow (c - 1 bit) window of the plan (window_geom)
   const uint32_t* keys = nullptr;
   const uint32_t* offsets = nullptr;
   void *buckets = nullptr, *pfirst = nullptr, *plast = nullptr, *nodes_a = nullptr, *nodes_b = nullptr;

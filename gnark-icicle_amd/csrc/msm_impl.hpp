@@ -60,8 +60,12 @@ GM_DEV FeG<Fr> load_scalar_canonical(const uint32_t* __restrict__ s, uint32_t i)
 // Plain layout: bucket b = w*nb + |d|-1 (window-major), entry value = point
 // index | sign << 31.  Precomputed (shared-bucket) layout: b = |d|-1 for every
 // window, value = w*stride + i (the shifted copy) | sign << 31.
-// Windows 0..wn-1 are c bits wide, windows wn..W-1 (the `narrow` windows of a
-// precomputed layout, msm.hpp MsmPrecomp) c - 1 bits; plain layouts: wn = W.
+// Windows 0..wn-1 are c bits wide, windows wn..W-1 (the `narrow` windows) c - 1
+// bits, with c W - narrow = bits + 1: no window is left with only the few top
+// bits of the scalar (precomputed layouts, msm.hpp MsmPrecomp, and plain
+// non-GLV layouts; a plain 2^24 BN254 MSM at c = 20 has 8 windows of 20 bits
+// and 5 of 19 instead of a 15-bit top window whose 2^14 buckets hold ~1024
+// points each -- spans of 16 slices that need the tree fixup).
 struct DigitGeom {
   uint32_t n, c, W, nb, shared_stride, F;  // F: pass-1 bin = b >> F
   uint32_t wn;
@@ -633,13 +637,23 @@ struct PairSel<Fe2<P, B>> {
   static constexpr auto seg() { return k_msm_seg_pair<P, B>; }
   static constexpr auto bitsum() { return k_msm_bitsum_pair<P, B>; }
 };
-// G2 runs on lane pairs unless GM_MSM_ACCUM=prefetch|noprefetch asks for the
-// one-lane kernels (A/B)
+// G2 runs on lane pairs.  The one-lane G2 kernels (a whole Fp2 point per lane;
+// they spill, and the BLS12-377 ones take minutes to compile) are built only
+// with -DGM_G2_ONE_LANE=1, and then GM_MSM_ACCUM=prefetch|noprefetch selects
+// them (A/B).
+#ifndef GM_G2_ONE_LANE
+#define GM_G2_ONE_LANE 0
+#endif
 inline bool g2_pairs() {
+  if (!GM_G2_ONE_LANE) return true;
   static const char* ov = getenv("GM_MSM_ACCUM");
   static const bool on = !(ov && (!strcmp(ov, "prefetch") || !strcmp(ov, "noprefetch")));
   return on;
 }
+// one-lane kernels instantiated for this field: always for G1, for G2 only
+// with GM_G2_ONE_LANE
+template <class F>
+constexpr bool kOneLane = !PairSel<F>::ok || GM_G2_ONE_LANE;
 
 // Full adds of the fixup / reduction kernels: lazily reduced for G1
 // (xyzz_add_lz, canonical on store), canonical xyzz_add otherwise.
@@ -925,6 +939,13 @@ int msm_plan(gm_ctx* ctx, Arena& arena, const void* scalars_dev, size_t n, const
   g.nb = plan.nb;
   g.shared_stride = shared ? (uint32_t)pre->stride : 0u;
   g.wn = shared ? W - pre->narrow : W;
+  if (!shared && !glv) {
+    // plain layout: balance the windows (see DigitGeom); GM_MSM_PLAIN_NARROW=0 keeps
+    // W full windows and a narrow top one (A/B)
+    static const bool narrow_on = !getenv("GM_MSM_PLAIN_NARROW") || atoi(getenv("GM_MSM_PLAIN_NARROW")) != 0;
+    const uint32_t narrow = c * W - (uint32_t)(plan.bits + 1);
+    if (narrow_on && narrow < W) g.wn = W - narrow;
+  }
   plan.wn = g.wn;
   g.F = sg.F + sg.G;  // the digits kernel counts pass-1 bins
   {
@@ -970,9 +991,11 @@ int msm_reduce(gm_ctx* ctx, MsmTail& t) {
       hipLaunchKernelGGL(PairSel<DF>::seg(), dim3(blocks_for(2 * (size_t)t.Wr * t.nseg, 128)), dim3(128), 0, st,
                          (const uint32_t*)t.buckets, t.nb, t.L, t.nseg, t.Wr, (uint32_t*)t.nodes_a);
   }
-  if (!pairs)
-    hipLaunchKernelGGL(k_msm_seg<DF>, dim3(blocks_for((size_t)t.Wr * t.nseg, 128)), dim3(128), 0, st,
-                       (const XYZZ<DF>*)t.buckets, t.nb, t.L, t.nseg, t.Wr, (XYZZ<DF>*)t.nodes_a);
+  if constexpr (kOneLane<DF>) {
+    if (!pairs)
+      hipLaunchKernelGGL(k_msm_seg<DF>, dim3(blocks_for((size_t)t.Wr * t.nseg, 128)), dim3(128), 0, st,
+                         (const XYZZ<DF>*)t.buckets, t.nb, t.L, t.nseg, t.Wr, (XYZZ<DF>*)t.nodes_a);
+  }
   // LDS tree levels until one node per window
   constexpr size_t SLOT_BUDGET = (96u << 10) / sizeof(XYZZ<DF>);
   uint32_t m = t.nseg;
@@ -993,9 +1016,11 @@ int msm_reduce(gm_ctx* ctx, MsmTail& t) {
         hipLaunchKernelGGL(PairSel<DF>::bitsum(), dim3(t.Wr * groups), dim3(BS_PAIR_THREADS), sizeof(XYZZ<DF>) * NT * Q,
                            st, (const uint32_t*)cur, m, Q, NT, lg, (uint32_t*)nxt);
     }
-    if (!pairs)
-      hipLaunchKernelGGL(k_msm_bitsum<DF>, dim3(t.Wr * groups), dim3(BS_THREADS), sizeof(XYZZ<DF>) * NT * Q, st,
-                         cur, m, Q, NT, lg, nxt);
+    if constexpr (kOneLane<DF>) {
+      if (!pairs)
+        hipLaunchKernelGGL(k_msm_bitsum<DF>, dim3(t.Wr * groups), dim3(BS_THREADS), sizeof(XYZZ<DF>) * NT * Q, st,
+                           cur, m, Q, NT, lg, nxt);
+    }
     Q += lg;
     m = groups;
     std::swap(cur, nxt);
@@ -1025,11 +1050,13 @@ int msm_fix_long(gm_ctx* ctx, MsmTail& t, uint32_t maxspan) {
       return GM_OK;
     }
   }
-  for (uint32_t d = 0; (1u << d) < maxspan; d++)
-    hipLaunchKernelGGL(k_msm_fix_tree<DF>, dim3(blocks_for(nslices, 128)), dim3(128), 0, st, t.keys, t.offsets,
-                       t.total, t.K, (uint32_t)nslices, d, (XYZZ<DF>*)t.pfirst);
-  hipLaunchKernelGGL(k_msm_fixup_long<DF>, dim3(blocks_for(t.total, 128)), dim3(128), 0, st, t.offsets, t.total,
-                     t.K, (XYZZ<DF>*)t.buckets, (const XYZZ<DF>*)t.pfirst, (const XYZZ<DF>*)t.plast);
+  if constexpr (kOneLane<DF>) {
+    for (uint32_t d = 0; (1u << d) < maxspan; d++)
+      hipLaunchKernelGGL(k_msm_fix_tree<DF>, dim3(blocks_for(nslices, 128)), dim3(128), 0, st, t.keys, t.offsets,
+                         t.total, t.K, (uint32_t)nslices, d, (XYZZ<DF>*)t.pfirst);
+    hipLaunchKernelGGL(k_msm_fixup_long<DF>, dim3(blocks_for(t.total, 128)), dim3(128), 0, st, t.offsets, t.total,
+                       t.K, (XYZZ<DF>*)t.buckets, (const XYZZ<DF>*)t.pfirst, (const XYZZ<DF>*)t.plast);
+  }
   GM_HIP(hipGetLastError());
   return GM_OK;
 }
@@ -1063,6 +1090,7 @@ int msm_launch(gm_ctx* ctx, Arena& arena, const MsmPlan& plan, const void* point
   if (plan.n == 0) return GM_OK;
   t.c = plan.c;
   t.W = plan.W;
+  t.wn = plan.wn;
   t.nb = plan.nb;
   t.total = plan.total;
   t.Wr = plan.Wred;
@@ -1120,16 +1148,18 @@ int msm_launch(gm_ctx* ctx, Arena& arena, const MsmPlan& plan, const void* point
     } else {
       pair = false;
     }
-    if (!pair) {
-      auto accum = prefetch ? k_msm_accum_seg_pf<DF> : (G2 ? k_msm_accum_seg_g2<DF> : k_msm_accum_seg_pf<DF>);
-      if constexpr (AccumW4<DF>::ok) {
-        if (!prefetch) accum = k_msm_accum_seg<DF>;
-        if (ov && !strcmp(ov, "idx")) accum = k_msm_accum_seg_idx<DF>;
+    if constexpr (kOneLane<DF>) {
+      if (!pair) {
+        auto accum = prefetch ? k_msm_accum_seg_pf<DF> : (G2 ? k_msm_accum_seg_g2<DF> : k_msm_accum_seg_pf<DF>);
+        if constexpr (AccumW4<DF>::ok) {
+          if (!prefetch) accum = k_msm_accum_seg<DF>;
+          if (ov && !strcmp(ov, "idx")) accum = k_msm_accum_seg_idx<DF>;
+        }
+        hipLaunchKernelGGL(accum, dim3(blocks_for(nslices, 128)), dim3(128), 0, st,
+                           reinterpret_cast<const uint32_t*>(points_internal), (uint32_t)plan.npts, plan.keys,
+                           plan.vals, plan.offsets, t.total, t.K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(),
+                           plast.as<XYZZ<DF>>(), errw.as<uint32_t>());
       }
-      hipLaunchKernelGGL(accum, dim3(blocks_for(nslices, 128)), dim3(128), 0, st,
-                         reinterpret_cast<const uint32_t*>(points_internal), (uint32_t)plan.npts, plan.keys,
-                         plan.vals, plan.offsets, t.total, t.K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(),
-                         plast.as<XYZZ<DF>>(), errw.as<uint32_t>());
     }
   }
   {
@@ -1143,10 +1173,12 @@ int msm_launch(gm_ctx* ctx, Arena& arena, const MsmPlan& plan, const void* point
         done = true;
       }
     }
-    if (!done)
-      hipLaunchKernelGGL(k_msm_fixup<DF>, dim3(blocks_for(t.total, 128)), dim3(128), 0, st, plan.offsets, t.total,
-                         t.K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>(),
-                         errw.as<uint32_t>() + 1);
+    if constexpr (kOneLane<DF>) {
+      if (!done)
+        hipLaunchKernelGGL(k_msm_fixup<DF>, dim3(blocks_for(t.total, 128)), dim3(128), 0, st, plan.offsets, t.total,
+                           t.K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>(),
+                           errw.as<uint32_t>() + 1);
+    }
   }
   // Bucket reduction, launched speculatively: buckets spanning more than
   // FIX_SERIAL slices (skewed scalars) are only known once errw[1] (max span)
@@ -1222,16 +1254,19 @@ int msm_finish(gm_ctx* ctx, MsmTail& t, typename GroupSel<C, G2>::HF (&jac_out)[
   std::vector<HF> hw(4 * (size_t)Wr * Q);
   memcpy(hw.data(), t.stage + 16, sizeof(HF) * hw.size());
   t.release_stage();  // the buffer may serve the next readback
-  // Host Horner over bit positions: window w contributes U_w at 2^(c w) and
-  // Y_{w,b} at 2^(c w + log2 L + b) (b < Q - 2 = log2(nseg), so every exponent
-  // stays below c (w + 1)).  Shared buckets: one window, w = 0.
+  // Host Horner over bit positions: window w (bit offset off_w, window_geom)
+  // contributes U_w at 2^off_w and Y_{w,b} at 2^(off_w + log2 L + b)
+  // (b < Q - 2 = log2(nseg), log2 L + log2 nseg = c - 1, so every exponent
+  // stays below the next window's offset).  Shared buckets: one window, w = 0.
   uint32_t lgL = 0;
   while ((1u << lgL) < t.L) lgL++;
   const int top = (int)(c * Wr);
   std::vector<std::vector<uint32_t>> at(top + 1);  // point ids per exponent
   for (uint32_t w = 0; w < Wr; w++) {
-    at[c * w].push_back(w * Q + 1);
-    for (uint32_t b = 0; b + 2 < Q; b++) at[c * w + lgL + b].push_back(w * Q + 2 + b);
+    uint32_t off, cw;
+    window_geom(c, Wr == 1 ? 1u : t.wn, w, off, cw);
+    at[off].push_back(w * Q + 1);
+    for (uint32_t b = 0; b + 2 < Q; b++) at[off + lgL + b].push_back(w * Q + 2 + b);
   }
   HJ acc = HJ::inf();
   for (int e = top; e >= 0; e--) {

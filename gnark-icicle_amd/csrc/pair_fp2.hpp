@@ -43,22 +43,26 @@ GM_DEV Fe<P> fe_select(bool c, const Fe<P>& a, const Fe<P>& b) {
   return r;
 }
 
-// Component of a * b (Fp2 = Fp[u]/(u^2 - BETA)), inputs < 4p per component,
-// result < 2p.
+// Component of a * b (Fp2 = Fp[u]/(u^2 - BETA)), inputs < 4p per component
+// with normalised limbs, result < 1.2p (BN254; ~p for BLS12-377).
+//   lane 0: a0 b0 + BETA a1 b1 = a.b + (5p - ap).(|BETA| bp)
+//   lane 1: a1 b0 + a0 b1      = a.bp + ap.b
+// Lane 0's subtraction is folded into its operand (carry-free 5p - ap), so
+// both lanes run ONE unsigned reduction of two products with the same
+// instructions: no per-lane sign select in every column, no + p pass and no
+// final conditional subtraction (the sum is < (16 + 20) p^2 / R' + p < 1.22p
+// for BN254, R' / p ~ 169).
 template <class P, int BETA>
 GM_DEV Fe<P> pf2_mul(const Fe<P>& a, const Fe<P>& b) {
   static_assert(BETA == -1 || BETA == -5, "unsupported non-residue");
   const bool odd = pair_odd();
   const Fe<P> ap = fe_swap(a), bp = fe_swap(b);
-  // lane 0: a0 b0 + BETA a1 b1 = a.b - |BETA| ap.bp;  lane 1: a1 b0 + a0 b1 = a.bp + ap.b
   Fe<P> y2 = odd ? b : bp;
   if constexpr (BETA == -5) {
     const Fe<P> b5 = fe_times5_lz(bp);  // < 20p, normalised limbs
     y2 = fe_select(odd, b, b5);
   }
-  Fe<P> r = fe_mul2_redc(a, fe_select(odd, bp, b), ap, y2, !odd);
-  fe_to2p<4>(r);
-  return r;
+  return fe_mul2_redc_u(a, fe_select(odd, bp, b), fe_select(odd, ap, fe_negk_cf<5>(ap)), y2);
 }
 
 // x1 y1 + x2 y2 - x3 y3 - x4 y4 + p in ONE Montgomery reduction (signed columns:
@@ -104,18 +108,32 @@ GM_DEV Fe<P> fe_mul4_redc(const Fe<P>& x1, const Fe<P>& y1, const Fe<P>& x2, con
   return r;
 }
 
+// Component of R W - Y PP (Fp2, BETA = -1) as ONE reduction of four products
+// per lane (fe_mul4_redc):
+//   lane 0: R0 W0 + Y1 P1 - R1 W1 - Y0 P0     lane 1: R1 W0 + R0 W1 - Y1 P0 - Y0 P1
+// Inputs normalised, R, W < 4p, Y, PP < 2p (negative side < 20 p^2 < p R');
+// result < 2.3p.  Used for Y3 of the mixed add and of the full add / doubling.
+template <class P>
+GM_DEV Fe<P> pf2_mul_sub(const Fe<P>& R, const Fe<P>& W, const Fe<P>& Y, const Fe<P>& PP) {
+  const bool odd = pair_odd();
+  const Fe<P> Rp = fe_swap(R), Wp = fe_swap(W), Yp = fe_swap(Y), Pp = fe_swap(PP);
+  return fe_mul4_redc(R, fe_select(odd, Wp, W), fe_select(odd, Rp, Yp), fe_select(odd, W, Pp),
+                      fe_select(odd, Y, Rp), fe_select(odd, Pp, Wp), fe_select(odd, Yp, Y), PP);
+}
+
 // Component of a^2, inputs < IN p per component, result < 2p.
 template <class P, int BETA, int IN>
 GM_DEV Fe<P> pf2_sqr(const Fe<P>& a) {
   if constexpr (BETA == -1) {
+    static_assert(IN <= 4, "pf2_sqr output bound (< 2p) needs inputs < 4p");
     // lane 0: (a0 + a1)(a0 - a1);  lane 1: 2 a1 a0
     const bool odd = pair_odd();
     const Fe<P> ap = fe_swap(a);
     const Fe<P> u = fe_add_lz(a, odd ? a : ap);
     const Fe<P> v = odd ? ap : fe_sub_lz<IN>(a, ap);
-    Fe<P> r = fe_mul_lz(u, v);  // u < 2 IN p, v < 2 IN p: (2 IN p)^2 <= 64 p^2 for IN <= 4
-    fe_to2p<4>(r);
-    return r;
+    // u < 2 IN p, v < 2 IN p: (2 IN p)^2 / R' + p < 1.4p for IN <= 4 (BN254
+    // R' / p ~ 169): already below 2p, no conditional subtraction
+    return fe_mul_lz(u, v);
   } else {
     return pf2_mul<P, BETA>(a, a);
   }
@@ -217,11 +235,7 @@ GM_DEV void pxyzz_add_aff(PXYZZ<P>& a, const Fe<P>& px, const Fe<P>& py_in, bool
   if constexpr (TRIM && BETA == -1) {
     // Y3 = R W - Y1 PPP (W = Q - X3) as ONE reduction of four products per lane:
     //   lane 0: R0 W0 + Y1 P1 - R1 W1 - Y0 P0     lane 1: R1 W0 + R0 W1 - Y1 P0 - Y0 P1
-    const Fe<P> W = fe_sub_lz<2>(Q, X3);                                       // < 4p
-    const bool odd = pair_odd();
-    const Fe<P> Rp = fe_swap(R), Wp = fe_swap(W), Yp = fe_swap(a.y), Pp = fe_swap(PPP);
-    Y3 = fe_mul4_redc(R, fe_select(odd, Wp, W), fe_select(odd, Rp, Yp), fe_select(odd, W, Pp),
-                      fe_select(odd, a.y, Rp), fe_select(odd, Pp, Wp), fe_select(odd, Yp, a.y), PPP);  // < 2.3p
+    Y3 = pf2_mul_sub(R, fe_sub_lz<2>(Q, X3), a.y, PPP);  // < 2.3p
   } else {
     Y3 = fe_sub_lz<2>(pf2_mul<P, BETA>(R, fe_sub_lz<2>(Q, X3)), pf2_mul<P, BETA>(a.y, PPP));  // < 4p
   }
@@ -375,7 +389,12 @@ GM_DEV PXYZZ<P> pxyzz_dbl(const PXYZZ<P>& a) {
   fe_to2p<8>(M);
   Fe<P> X3 = fe_sub_lz<4>(pf2_sqr<P, BETA, 2>(M), fe_add_lz(S, S));  // < 6p
   fe_to2p<8>(X3);
-  const Fe<P> Y3 = fe_sub_lz<2>(pf2_mul<P, BETA>(M, fe_sub_lz<2>(S, X3)), pf2_mul<P, BETA>(Wv, a.y));  // < 4p
+  Fe<P> Y3;  // M (S - X3) - Wv Y1
+  if constexpr (BETA == -1 && P::N <= 9) {
+    Y3 = pf2_mul_sub(M, fe_sub_lz<2>(S, X3), Wv, a.y);  // < 2.3p: one reduction of four products
+  } else {
+    Y3 = fe_sub_lz<2>(pf2_mul<P, BETA>(M, fe_sub_lz<2>(S, X3)), pf2_mul<P, BETA>(Wv, a.y));  // < 4p
+  }
   PXYZZ<P> r;
   r.x = fe_canon<1>(X3);
   r.y = fe_canon<2>(Y3);
@@ -404,7 +423,12 @@ GM_DEV PXYZZ<P> pxyzz_add(const PXYZZ<P>& a, const PXYZZ<P>& b) {
   const Fe<P> Q = pf2_mul<P, BETA>(U1, PP);
   Fe<P> X3 = fe_sub_lz<4>(fe_sub_lz<2>(pf2_sqr<P, BETA, 4>(R), PPP), fe_add_lz(Q, Q));  // < 8p
   fe_to2p<8>(X3);
-  const Fe<P> Y3 = fe_sub_lz<2>(pf2_mul<P, BETA>(R, fe_sub_lz<2>(Q, X3)), pf2_mul<P, BETA>(S1, PPP));  // < 4p
+  Fe<P> Y3;  // R (Q - X3) - S1 PPP
+  if constexpr (BETA == -1 && P::N <= 9) {
+    Y3 = pf2_mul_sub(R, fe_sub_lz<2>(Q, X3), S1, PPP);  // < 2.3p: one reduction of four products
+  } else {
+    Y3 = fe_sub_lz<2>(pf2_mul<P, BETA>(R, fe_sub_lz<2>(Q, X3)), pf2_mul<P, BETA>(S1, PPP));  // < 4p
+  }
   PXYZZ<P> r;
   r.x = fe_canon<1>(X3);
   r.y = fe_canon<2>(Y3);
