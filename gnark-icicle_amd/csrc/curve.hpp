@@ -147,9 +147,10 @@ GM_DEV void xyzz_add_aff_lz(XYZZ<Fe<P>>& a, const Affine<Fe<P>>& p, bool neg) {
   F Q = fe_mul_lz(a.x, PP);                          // < 2p
   a.zzz = fe_mul_lz(a.zzz, PPP);
   F X3 = fe_sub2x_lz<6>(fe_sqr_lz(R), PPP, Q);       // R^2 - PPP - 2Q + 6p < 8p
-  // R (< 6p) * (Q - X3 + 8p < 10p) - Y1 (< 4p) * PPP (< 2p), one reduction:
-  // < 60 p^2 / R' + 2p < 2.4p (x2 y2 = 8 p^2 < R' p as fe_mul2_redc needs)
-  a.y = fe_mul2_redc(R, fe_sub_lz<8>(Q, X3), a.y, PPP, true);
+  // R (< 6p) * (Q - X3 + 8p < 10p) + (5p - Y1) (Y1 < 4p) * PPP (< 2p), ONE unsigned
+  // reduction (fe_mul2_redc_u; Y1's negation folded into the carry-free operand
+  // 5p - Y1, so no signed columns and no + p pass): < 70 p^2 / R' + p < 1.5p
+  a.y = fe_mul2_redc_u(R, fe_sub_lz<8>(Q, X3), fe_negk_cf<5>(a.y), PPP);
   a.x = X3;
 }
 // Lazily reduced a += p for G2 buckets (Fp2 coordinates).  Invariants: every
@@ -279,9 +280,9 @@ GM_DEV XYZZ<Fe<P>> xyzz_add_lz(const XYZZ<Fe<P>>& a, const XYZZ<Fe<P>>& b) {
   const F Q = fe_mul_lz(U1, PP);
   F X3 = fe_sub_lz<4>(fe_sub_lz<2>(fe_sqr_lz(R), PPP), fe_add_lz(Q, Q));  // < 8p
   fe_to2p<8>(X3);
-  // R (< 4p) (Q - X3 + 2p < 4p) - S1 PPP (< 4 p^2 < R' p), one reduction: < 2.1p
-  F Y3 = fe_mul2_redc(R, fe_sub_lz<2>(Q, X3), S1, PPP, true);
-  fe_to2p<4>(Y3);
+  // R (< 4p) (Q - X3 + 2p < 4p) + (3p - S1) PPP (S1 < 1.1p, PPP < 2p), one unsigned
+  // reduction: < 22 p^2 / R' + p < 1.2p, below 2p without a subtraction
+  const F Y3 = fe_mul2_redc_u(R, fe_sub_lz<2>(Q, X3), fe_negk_cf<3>(S1), PPP);
   XYZZ<F> r;
   r.x = X3;
   r.y = Y3;

@@ -370,57 +370,11 @@ template <class P>
 GM_DEV Fe<P> fe_mul_lz_chain(const Fe<P>& a, const Fe<P>& b) { return fe_mul<P, false, true>(a, b); }
 template <class P>
 GM_DEV Fe<P> fe_sqr_lz(const Fe<P>& a) { return fe_sqr<P, false>(a); }
-// Montgomery reduction of x1*y1 + (neg ? -1 : 1) * x2*y2 (radix 2^29 product
-// scanning, one 64-bit column accumulator): signed columns when neg (arithmetic
-// shifts), unsigned otherwise.  All inputs have normalised limbs; |column| stays
-// below 2^63 (N = 9: 2^62.2, N = 14: 2^62.8 signed, 2^63.4 unsigned).  With neg,
-// p is added to the result, which makes it non-negative for x2*y2 < p R'.
-// Output < x1*y1 / R' + p (+ p when neg).
-// Used by the G1 lazy add (Y3 = R (Q - X3) - Y1 PPP: one reduction instead of two)
-// and by the lane-pair Fp2 products (pair_fp2.hpp).
-template <class P>
-GM_DEV Fe<P> fe_mul2_redc(const Fe<P>& x1, const Fe<P>& y1, const Fe<P>& x2, const Fe<P>& y2, bool neg) {
-  constexpr int N = P::N;
-  uint32_t m[N];
-  Fe<P> r;
-  uint64_t acc = 0;
-#pragma unroll
-  for (int k = 0; k < 2 * N - 1; k++) {
-    uint64_t c1 = 0, c2 = 0;
-#pragma unroll
-    for (int i = (k - N + 1 > 0 ? k - N + 1 : 0); i <= (k < N - 1 ? k : N - 1); i++) {
-      c1 += (uint64_t)x1.v[i] * y1.v[k - i];
-      c2 += (uint64_t)x2.v[i] * y2.v[k - i];
-    }
-    acc += c1 + (neg ? (uint64_t)0 - c2 : c2);
-#pragma unroll
-    for (int i = (k - N + 1 > 0 ? k - N + 1 : 0); i <= (k - 1 < N - 1 ? k - 1 : N - 1); i++)
-      acc += (uint64_t)m[i] * P::p(k - i);
-    if (k < N) {
-      m[k] = ((uint32_t)acc * P::INV) & LIMB_MASK;
-      acc += (uint64_t)m[k] * P::p(0);
-    } else {
-      r.v[k - N] = (uint32_t)acc & LIMB_MASK;
-    }
-    acc = neg ? (uint64_t)((int64_t)acc >> RADIX) : acc >> RADIX;
-  }
-  r.v[N - 1] = (uint32_t)acc;  // two's complement top limb when negative
-  // + p where neg (the sum is then >= 0; the top limb wraps back to positive)
-  uint32_t c = 0;
-  const uint32_t msk = neg ? 0xffffffffu : 0u;
-#pragma unroll
-  for (int i = 0; i < N; i++) {
-    const uint32_t s = r.v[i] + (P::p(i) & msk) + c;
-    r.v[i] = i == N - 1 ? s : (s & LIMB_MASK);
-    c = s >> RADIX;
-  }
-  return r;
-}
-
 // Unsigned Montgomery reduction of x1*y1 + x2*y2 (radix 2^29 product scanning,
-// one 64-bit column accumulator, no per-lane sign): the lane-pair Fp2 product
-// negates its second operand up front (fe_negk_cf) instead of subtracting the
-// product, so both lanes of a pair run the same instructions.  Column bound:
+// one 64-bit column accumulator, no signs).  A difference x1 y1 - x y2 is
+// computed as x1 y1 + (K p - x) y2 with the carry-free operand fe_negk_cf<K>(x):
+// the G1 add's Y3 = R (Q - X3) - Y1 PPP (one reduction instead of two), and the
+// lane-pair Fp2 product, whose two lanes then run the same instructions.  Column bound:
 // N (2^58 + 2^59 + 2^58) < 2^64 for N <= 14 with x1, y1, y2 normalised and x2
 // limbs < 2^30.  Output < (x1 y1 + x2 y2) / R' + p, limbs normalised.
 template <class P>
