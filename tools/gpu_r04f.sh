@@ -22,3 +22,11 @@ python3 -c "
 import json; d=json.load(open('gpurun_out/${T}_bench.json')); print(d['value'], d['ms_per_step'], d['kernel_avg_ms']); s=d['secondary']
 print(json.dumps(s['msm']))
 for g in s['groth16']: print(g['logn'], g['pk'], g['prove_ms_host_inputs'], g['prove_ms_device_inputs'], g['prove_ms_r1cs_resident'])"
+# host-input Groth16 2^24 (precomputed): staged pinned ring vs pageable hipMemcpyAsync, same box
+for v in staged pageable staged pageable; do
+  if [ $v = pageable ]; then export GM_H2D=pageable; else unset GM_H2D; fi
+  timeout -k 10 400 python3 bench.py --no-cpu-baseline --steps 1 --warmup 1 --g16-logn 24 --g16-plain "" --msm-extra 0 --ntt-logn 20 > gpurun_out/${T}_h2d_$v.json 2> gpurun_out/${T}_h2d_$v.err || { tail -20 gpurun_out/${T}_h2d_$v.err; exit 1; }
+  python3 -c "
+import json; g=json.load(open('gpurun_out/${T}_h2d_$v.json'))['secondary']['groth16'][0]; print('$v', g['prove_ms_host_inputs'], g['prove_ms_device_inputs'], g['prove_ms_r1cs_resident'])"
+done
+unset GM_H2D
