@@ -43,8 +43,8 @@ G16_BYTES_PER_ELEM = 4 * 96 + 160 + 7 * 64 + 128
 # committed rocprofv3 --pmc summaries the roofline's traffic / valu fields are
 # read from (collected by tools/gpu_pmc.sh / tools/pmc_traffic.py on the bench's
 # own MSM workload; NOT measured inside this run)
-PMC_TRAFFIC_FILE = "profiles/r03h_pmc_traffic.json"
-PMC_VALU_FILE = "profiles/r03h_pmc_valu.json"
+PMC_TRAFFIC_FILE = "profiles/r04g_pmc_traffic.json"
+PMC_VALU_FILE = "profiles/r04g_pmc_valu.json"
 
 
 def parse():
@@ -198,8 +198,8 @@ def main():
         "valu": load_pmc_valu("k_msm_accum_seg<Fe<Bn254Fp> >"),
         "valu_source": PMC_VALU_FILE + " (rocprofv3 --pmc SQ_* passes; committed profile, not measured in this run)",
         "note": "bound=hbm is the bench contract's roofline for this non-MFMA path; the kernel is NOT HBM-bound: "
-                "its binding resource is VALU issue -- rocprofv3 PMC (profiles/r03h_pmc_valu.json) shows VALUBusy "
-                "~0.87 (gfx9 formula, 4 cycles/instr) for k_msm_accum_seg, ~2560 VALU instructions per mixed add; "
+                "its binding resource is VALU issue -- rocprofv3 PMC (" + PMC_VALU_FILE + ") shows VALUBusy "
+                "~0.87 (gfx9 formula, 4 cycles/instr) for k_msm_accum_seg, ~2510 VALU instructions per mixed add; "
                 "int_alu prices the v_mad_u64_u32 work at the measured mad-only issue peak (DESIGN.md section 3)",
     }
     kernel_ms = {k: round(v[0] / max(v[1], 1), 4) for k, v in stats.items()}

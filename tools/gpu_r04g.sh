@@ -1,10 +1,21 @@
 #!/bin/bash
-# r04g: round-4 evidence -- rocprofv3 kernel stats of the default bench line, VALU counter passes
-# over the 2^20 G1 MSM, the 2^20 G2 MSM and the 2^24 NTT, FETCH / WRITE traffic passes over the G1 MSM.
+# r04g: growing-bound DIF rounds (GM_NTT_GROW) parity + same-box A/B, the FP64-limb Montgomery
+# microbench, then round-4 evidence -- rocprofv3 kernel stats of the default bench line, VALU counter
+# passes over the 2^20 G1 MSM, the 2^20 G2 MSM and the 2^24 NTT, FETCH / WRITE traffic over the G1 MSM.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out && export TMPDIR=/tmp
 T=${1:-r04g}
+timeout -k 10 600 python -u -m pytest tests/test_ntt_gpu.py tests/test_golden_gpu.py tests/test_configs_full.py tests/test_groth16_gpu.py tests/test_icicle_replay_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/${T}_tests.log 2>&1 || { tail -40 gpurun_out/${T}_tests.log; exit 1; }
+tail -1 gpurun_out/${T}_tests.log
+for rep in 1 2 3; do
+  for g in 1 0; do
+    for args in "--logn 24" "--logn 24 --coset" "--curve bls12377 --logn 22" "--logn 20"; do
+      echo -n "grow=$g $args: "; GM_NTT_GROW=$g timeout -k 10 120 python3 tools/ntt_only.py $args || exit 1
+    done
+  done
+done 2>&1 | tee gpurun_out/${T}_ntt_grow_ab.txt | cut -c1-150
+/opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -o /tmp/fp64mont tools/microbench/fp64mont.hip && timeout -k 10 60 /tmp/fp64mont /tmp/fp64mont_dump.txt > gpurun_out/${T}_fp64mont.txt 2>&1 && python3 tools/microbench/fp64mont_check.py /tmp/fp64mont_dump.txt >> gpurun_out/${T}_fp64mont.txt; cat gpurun_out/${T}_fp64mont.txt
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_prof -o prof -- python3 bench.py --no-cpu-baseline --no-secondary > gpurun_out/${T}_profbench.json 2> gpurun_out/${T}_prof.err || { tail -30 gpurun_out/${T}_prof.err; exit 1; }
 python3 tools/prof_summary.py $(ls gpurun_out/${T}_prof/*kernel_stats.csv gpurun_out/${T}_prof/*/*kernel_stats.csv 2>/dev/null | head -1) > gpurun_out/${T}_rocprof_summary.txt
 head -12 gpurun_out/${T}_rocprof_summary.txt
