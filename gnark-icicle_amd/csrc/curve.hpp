@@ -147,10 +147,16 @@ GM_DEV void xyzz_add_aff_lz(XYZZ<Fe<P>>& a, const Affine<Fe<P>>& p, bool neg) {
   F Q = fe_mul_lz(a.x, PP);                          // < 2p
   a.zzz = fe_mul_lz(a.zzz, PPP);
   F X3 = fe_sub2x_lz<6>(fe_sqr_lz(R), PPP, Q);       // R^2 - PPP - 2Q + 6p < 8p
-  // R (< 6p) * (Q - X3 + 8p < 10p) + (5p - Y1) (Y1 < 4p) * PPP (< 2p), ONE unsigned
+  // R (< 6p) * (Q - X3 + 9p < 11p) + (5p - Y1) (Y1 < 4p) * PPP (< 2p), ONE unsigned
   // reduction (fe_mul2_redc_u; Y1's negation folded into the carry-free operand
-  // 5p - Y1, so no signed columns and no + p pass): < 70 p^2 / R' + p < 1.5p
-  a.y = fe_mul2_redc_u(R, fe_sub_lz<8>(Q, X3), fe_negk_cf<5>(a.y), PPP);
+  // 5p - Y1, so no signed columns and no + p pass): < 76 p^2 / R' + p < 1.5p.
+  // Q - X3 + 9p is carry-free too (fe_sub_cf, limbs < 3 2^29) where the columns
+  // hold it: N (3 + 2 + 1) 2^58 < 2^64 for N <= 10 (BN254; BLS12-377's 13 limbs
+  // take the normalised difference)
+  if constexpr (P::N <= 10)
+    a.y = fe_mul2_redc_u(R, fe_sub_cf<9>(Q, X3), fe_negk_cf<5>(a.y), PPP);
+  else
+    a.y = fe_mul2_redc_u(R, fe_sub_lz<8>(Q, X3), fe_negk_cf<5>(a.y), PPP);
   a.x = X3;
 }
 // Lazily reduced a += p for G2 buckets (Fp2 coordinates).  Invariants: every

@@ -268,7 +268,10 @@ GM_DEV Fe<P> fe_neg(const Fe<P>& a) {
 // and adding the carry with a 64-bit add, v_lshl_add_u64, per column).  One
 // dependent mad chain per product: for kernels with several independent
 // products in flight per thread (the radix-4 NTT rounds).
-template <class P, bool REDUCE = true, bool CHAIN = false>
+#ifndef GM_FE_CHAIN
+#define GM_FE_CHAIN 0
+#endif
+template <class P, bool REDUCE = true, bool CHAIN = GM_FE_CHAIN>
 GM_DEV Fe<P> fe_mul(const Fe<P>& a, const Fe<P>& b) {
   constexpr int N = P::N;
   uint32_t m[N];
@@ -307,6 +310,9 @@ GM_DEV Fe<P> fe_sqr(const Fe<P>& a) {
   uint64_t acc = 0;
 #pragma unroll
   for (int k = 0; k < 2 * N - 1; k++) {
+    if constexpr (GM_FE_CHAIN) {
+      if (k) __asm__ volatile("" : "+v"(acc));
+    }
     uint64_t cross = 0;
 #pragma unroll
     for (int i = (k - N + 1 > 0 ? k - N + 1 : 0); i <= (k < N - 1 ? k : N - 1); i++) {
@@ -386,6 +392,9 @@ GM_DEV Fe<P> fe_mul2_redc_u(const Fe<P>& x1, const Fe<P>& y1, const Fe<P>& x2, c
   uint64_t acc = 0;
 #pragma unroll
   for (int k = 0; k < 2 * N - 1; k++) {
+    if constexpr (GM_FE_CHAIN) {
+      if (k) __asm__ volatile("" : "+v"(acc));
+    }
 #pragma unroll
     for (int i = (k - N + 1 > 0 ? k - N + 1 : 0); i <= (k < N - 1 ? k : N - 1); i++) {
       acc += (uint64_t)x1.v[i] * y1.v[k - i];
@@ -471,6 +480,19 @@ GM_DEV Fe<P> fe_negk_cf(const Fe<P>& s) {
   Fe<P> r;
 #pragma unroll
   for (int i = 0; i < P::N; i++) r.v[i] = kp_borrowed_limb<P, K>(i) - s.v[i];
+  return r;
+}
+// a - b + K p as a product operand only, carry-free (two VOP2 per limb instead of
+// fe_sub_lz's signed carry pass): a, b normalised, b < (K - 1) p.  The limbs are
+// left unnormalised, < 3 2^29, which a Montgomery product's 64-bit columns
+// absorb next to a normalised second operand (9 N 2^58 + N 2^58 < 2^64 for
+// N <= 11); the value, < a + K p, is what fe_sub_lz<K> returns.
+template <int K, class P>
+GM_DEV Fe<P> fe_sub_cf(const Fe<P>& a, const Fe<P>& b) {
+  static_assert(P::N <= 11, "unnormalised product operand column bound");
+  Fe<P> r;
+#pragma unroll
+  for (int i = 0; i < P::N; i++) r.v[i] = a.v[i] + (kp_borrowed_limb<P, K>(i) - b.v[i]);
   return r;
 }
 // neg ? 2p - s : s for s < 2p with normalised limbs, carry-free (2 VOP2 per limb

@@ -288,6 +288,14 @@ __global__ void __launch_bounds__(TPB) k_ntt_pass(Fe<P>* __restrict__ data, int 
 #ifndef NTT_R4_WPE
 #define NTT_R4_WPE 1
 #endif
+// round twiddles of the DIF pass fetched one round ahead (k_ntt_pass4)
+#ifndef NTT_TW_PF
+#define NTT_TW_PF 1
+#endif
+// the DIF kernel (inter-pass twiddles on the store) separately: -DNTT_DIF_WPE=3
+#ifndef NTT_DIF_WPE
+#define NTT_DIF_WPE NTT_R4_WPE
+#endif
 
 // f(0), f(1), f(2), f(3) with compile-time indices (register-resident arrays)
 template <class F>
@@ -303,24 +311,26 @@ GM_DEV Fe<P> ntt_tw(const Fe<P>* __restrict__ sub, int i) {
   return sub[i];
 }
 
-// products of a round: one mad chain each (CH) or the compiler's split columns
+// products of a round: one mad chain each (CH) or the compiler's split columns.
+// A difference that only feeds a product is formed carry-free (fe_sub_cf: value
+// below a + K p with K one above fe_sub_lz's, every product input < 33 p^2 < R' p).
 #define MUL(x, y) (CH ? fe_mul_lz_chain(x, y) : fe_mul_lz(x, y))
 // DIF radix-2 butterfly pair of one round: (u, v) -> (u + v, (u - v + Kp) w)
 template <class P, bool CH>
 GM_DEV void r4_dif(Fe<P> (&e)[4], const Fe<P>& t1, const Fe<P>& t2, const Fe<P>& t3) {
   // stage lm: (e0, e2) by w_2m^jj, (e1, e3) by w_2m^(jj+s); inputs < 2p
   const Fe<P> s0 = fe_add_lz(e[0], e[2]);                        // < 4p
-  const Fe<P> d0 = MUL(fe_sub_lz<2>(e[0], e[2]), t1);      // < 2p
+  const Fe<P> d0 = MUL(fe_sub_cf<3>(e[0], e[2]), t1);      // < 2p
   const Fe<P> s1 = fe_add_lz(e[1], e[3]);                        // < 4p
-  const Fe<P> d1 = MUL(fe_sub_lz<2>(e[1], e[3]), t2);      // < 2p
+  const Fe<P> d1 = MUL(fe_sub_cf<3>(e[1], e[3]), t2);      // < 2p
   // stage lm - 1: (s0, s1), (d0, d1) by w_m^jj
   e[0] = fe_add_lz(s0, s1);                                      // < 8p
   fe_reduce_k<4>(e[0]);
   fe_reduce_k<2>(e[0]);                                          // < 2p
-  e[1] = MUL(fe_sub_lz<4>(s0, s1), t3);                    // < 2p
+  e[1] = MUL(fe_sub_cf<5>(s0, s1), t3);                    // < 2p
   e[2] = fe_add_lz(d0, d1);                                      // < 4p
   fe_reduce_k<2>(e[2]);                                          // < 2p
-  e[3] = MUL(fe_sub_lz<2>(d0, d1), t3);                    // < 2p
+  e[3] = MUL(fe_sub_cf<3>(d0, d1), t3);                    // < 2p
 }
 // the s = 1 DIF round (twiddles 1, w_4, 1): inputs < 2p, outputs < 8p
 template <class P, bool CH>
@@ -328,11 +338,40 @@ GM_DEV void r4_dif_w4(Fe<P> (&e)[4], const Fe<P>& w4) {
   const Fe<P> s0 = fe_add_lz(e[0], e[2]);                        // < 4p
   const Fe<P> d0 = fe_sub_lz<2>(e[0], e[2]);                     // < 4p
   const Fe<P> s1 = fe_add_lz(e[1], e[3]);                        // < 4p
-  const Fe<P> d1 = MUL(fe_sub_lz<2>(e[1], e[3]), w4);      // < 2p
+  const Fe<P> d1 = MUL(fe_sub_cf<3>(e[1], e[3]), w4);      // < 2p
   e[0] = fe_add_lz(s0, s1);                                      // < 8p
   e[1] = fe_sub_lz<4>(s0, s1);                                   // < 8p
   e[2] = fe_add_lz(d0, d1);                                      // < 6p
   e[3] = fe_sub_lz<2>(d0, d1);                                   // < 6p
+}
+// DIF rounds of a pass that is not the last one (lo > 0, even t): bounds grow
+// instead of every sum being reduced -- round R takes inputs < B p (B = 2^(R+1))
+// and reduces only e0 (one conditional subtraction per round instead of three);
+// the products (< 2p) reset the other lanes.  The last (w_4) round's outputs,
+// < 64p at t = 8, go straight into the inter-pass twiddle product of the store
+// (64 p^2 < R' p).
+template <class P, bool CH, int B>
+GM_DEV void r4_dif_grow(Fe<P> (&e)[4], const Fe<P>& t1, const Fe<P>& t2, const Fe<P>& t3) {
+  const Fe<P> s0 = fe_add_lz(e[0], e[2]);                        // < 2B p
+  const Fe<P> d0 = MUL(fe_sub_cf<B + 1>(e[0], e[2]), t1);        // < 2p
+  const Fe<P> s1 = fe_add_lz(e[1], e[3]);                        // < 2B p
+  const Fe<P> d1 = MUL(fe_sub_cf<B + 1>(e[1], e[3]), t2);        // < 2p
+  e[0] = fe_add_lz(s0, s1);                                      // < 4B p
+  fe_reduce_k<2 * B>(e[0]);                                      // < 2B p
+  e[1] = MUL(fe_sub_cf<2 * B + 1>(s0, s1), t3);                  // < 2p (value < (4B + 1) p)
+  e[2] = fe_add_lz(d0, d1);                                      // < 4p
+  e[3] = MUL(fe_sub_cf<3>(d0, d1), t3);                          // < 2p
+}
+template <class P, bool CH, int B>
+GM_DEV void r4_dif_w4_grow(Fe<P> (&e)[4], const Fe<P>& w4) {
+  const Fe<P> s0 = fe_add_lz(e[0], e[2]);                        // < 2B p
+  const Fe<P> d0 = fe_sub_lz<B>(e[0], e[2]);                     // < 2B p
+  const Fe<P> s1 = fe_add_lz(e[1], e[3]);                        // < 2B p
+  const Fe<P> d1 = MUL(fe_sub_cf<B + 1>(e[1], e[3]), w4);        // < 2p
+  e[0] = fe_add_lz(s0, s1);                                      // < 4B p
+  e[1] = fe_sub_lz<2 * B>(s0, s1);                               // < 4B p
+  e[2] = fe_add_lz(d0, d1);                                      // < (2B + 2) p
+  e[3] = fe_sub_lz<2>(d0, d1);                                   // < (2B + 2) p
 }
 // DIT (Harvey) round: (u, v) -> (u + v w, u - v w + 2p); inputs < 4p, outputs < 4p
 template <class P, bool CH>
@@ -345,7 +384,7 @@ GM_DEV void r4_dit(Fe<P> (&e)[4], const Fe<P>& a, const Fe<P>& b, const Fe<P>& c
   Fe<P> s0 = fe_add_lz(e[0], v1);                                // < 4p
   Fe<P> s1 = fe_sub_lz<2>(e[0], v1);
   const Fe<P> s2 = fe_add_lz(e[2], v3);
-  const Fe<P> s3 = fe_sub_lz<2>(e[2], v3);
+  const Fe<P> s3 = fe_sub_cf<3>(e[2], v3);                       // product operand only
   // stage lm + 1: (s0, s2) by w_4m^jj, (s1, s3) by w_4m^(jj+s)
   fe_reduce_k<2>(s0);
   fe_reduce_k<2>(s1);
@@ -362,7 +401,7 @@ GM_DEV void r4_dit_w4(Fe<P> (&e)[4], const Fe<P>& w4) {
   const Fe<P> s0 = fe_add_lz(e[0], e[1]);                        // < 4p
   const Fe<P> s1 = fe_sub_lz<2>(e[0], e[1]);                     // < 4p
   const Fe<P> s2 = fe_add_lz(e[2], e[3]);                        // < 4p
-  const Fe<P> y = MUL(fe_sub_lz<2>(e[2], e[3]), w4);       // < 2p
+  const Fe<P> y = MUL(fe_sub_cf<3>(e[2], e[3]), w4);       // < 2p
   e[0] = fe_add_lz(s0, s2);                                      // < 8p
   e[2] = fe_sub_lz<4>(s0, s2);                                   // < 8p
   e[1] = fe_add_lz(s1, y);                                       // < 6p
@@ -372,8 +411,26 @@ GM_DEV void r4_dit_w4(Fe<P> (&e)[4], const Fe<P>& w4) {
 
 #undef MUL
 
+// twiddles of a round whose lower stage is ls: w_4 for ls = 0, else DIF
+// (t1, t2, t3) / DIT (a, b, c) of the thread's group k
+template <class P, bool DIT>
+GM_DEV void r4_fetch_tw(const Fe<P>* __restrict__ sub, int t, int ls, int k, Fe<P>& tw0, Fe<P>& tw1, Fe<P>& tw2) {
+  const int sr = 1 << ls, jj = k & (sr - 1);
+  if (sr == 1) {
+    tw0 = tw1 = tw2 = ntt_tw(sub, 1 << (t - 2));  // all three written: nothing stays live across rounds
+  } else if (!DIT) {
+    tw0 = ntt_tw(sub, jj << (t - ls - 2));
+    tw1 = ntt_tw(sub, (jj + sr) << (t - ls - 2));
+    tw2 = ntt_tw(sub, jj << (t - ls - 1));
+  } else {
+    tw0 = ntt_tw(sub, jj << (t - ls - 1));
+    tw1 = ntt_tw(sub, jj << (t - ls - 2));
+    tw2 = ntt_tw(sub, (jj + sr) << (t - ls - 2));
+  }
+}
+
 template <class P, bool DIT, bool CH = false>
-__global__ void __launch_bounds__(NTT_TPB) __attribute__((amdgpu_waves_per_eu(NTT_R4_WPE))) k_ntt_pass4(Fe<P>* __restrict__ data, int logn, int lo, int t,
+__global__ void __launch_bounds__(NTT_TPB) __attribute__((amdgpu_waves_per_eu(DIT ? NTT_R4_WPE : NTT_DIF_WPE))) k_ntt_pass4(Fe<P>* __restrict__ data, int logn, int lo, int t, bool ntt_grow,
                                                        const Fe<P>* __restrict__ tw,
                                                        const Fe<P>* __restrict__ sub,
                                                        const Fe<P>* __restrict__ pre,
@@ -393,6 +450,10 @@ __global__ void __launch_bounds__(NTT_TPB) __attribute__((amdgpu_waves_per_eu(NT
   const size_t lomask = ((size_t)1 << lo) - 1;
   const size_t base = ((o >> lo) << (lo + t)) + (o & lomask);  // (j, ol) lives at base + (j << lo)
   const bool last_pass = DIT ? (lo + t == logn) : (lo == 0);
+  // growing DIF bounds (r4_dif_grow): passes whose store multiplies every element
+  // by an inter-pass twiddle, with no lone radix-2 stage (it takes inputs < 2p);
+  // GM_NTT_GROW=0 keeps every round's outputs < 2p (A/B)
+  const bool grow = !DIT && lo > 0 && !(t & 1) && ntt_grow;
   // rounds: DIF stages (t-1, t-2), (t-3, t-4), ...; DIT (0, 1), (2, 3), ...
   const int nr = t >> 1;
   auto quarter = [&](int r) { return DIT ? 2 * r : t - 2 - 2 * r; };  // ls of round r
@@ -408,12 +469,20 @@ __global__ void __launch_bounds__(NTT_TPB) __attribute__((amdgpu_waves_per_eu(NT
     unroll4([&](auto I) {
       const size_t addr = base + ((size_t)(j0 + I * s) << lo);
       Fe<P> v = ld_fe(data, addr);
-      if (pb) v = fe_sub(fe_mul(v, fe_to_internal(ld_fe(pb, addr))), ld_fe(pc, addr));
-      if (pre) v = fe_mul(v, ld_tab(pre, addr));
-      if (DIT && lo > 0) v = fe_mul_lz(v, ld_tab(tw, ((size_t)(j0 + I * s) << lo) + (o & lomask)));  // < 2p
+      if (pb) v = fe_sub(fe_mul<P, true, CH>(v, fe_to_internal(ld_fe(pb, addr))), ld_fe(pc, addr));
+      if (pre) v = fe_mul<P, true, CH>(v, ld_tab(pre, addr));
+      if (DIT && lo > 0) v = fe_mul<P, false, CH>(v, ld_tab(tw, ((size_t)(j0 + I * s) << lo) + (o & lomask)));  // < 2p
       e[I] = v;
     });
   }
+  // twiddles of round r: tw0 = w_4 for the s = 1 round, else DIF (t1, t2, t3) /
+  // DIT (a, b, c).  The DIF pass (two waves per SIMD) fetches them one round
+  // ahead, before the tile exchange, so their L2 latency overlaps the barriers
+  // (NTT_TW_PF=0: fetched after the exchange, A/B); the DIT pass runs at four
+  // waves and keeps the registers.
+  Fe<P> tw0, tw1, tw2;
+  constexpr bool tw_ahead = !DIT && NTT_TW_PF;
+  if (tw_ahead && nr > 0) r4_fetch_tw<P, DIT>(sub, t, quarter(0), k, tw0, tw1, tw2);
   for (int r = 0; r < nr; r++) {
     if (r > 0) {
       // exchange through the tile: this round's elements of every thread
@@ -423,17 +492,62 @@ __global__ void __launch_bounds__(NTT_TPB) __attribute__((amdgpu_waves_per_eu(NT
       place(r);
       unroll4([&](auto I) { e[I] = X[(j0 + I * s) * B + ol]; });
     }
-    const int ls = quarter(r);
-    const int jj = k & (s - 1);
-    if (s == 1) {  // block-uniform
-      const Fe<P> w4 = ntt_tw(sub, 1 << (t - 2));
-      if (DIT) r4_dit_w4<P, CH>(e, w4);
-      else r4_dif_w4<P, CH>(e, w4);
-    } else if (!DIT) {
-      r4_dif<P, CH>(e, ntt_tw(sub, jj << (t - ls - 2)), ntt_tw(sub, (jj + s) << (t - ls - 2)), ntt_tw(sub, jj << (t - ls - 1)));
+    if constexpr (tw_ahead) {
+      if (grow) {  // lo > 0, even t (block-uniform): round r takes inputs < 2^(r+1) p
+        if (s == 1) {
+          switch (r) {
+            case 0: r4_dif_w4_grow<P, CH, 2>(e, tw0); break;
+            case 1: r4_dif_w4_grow<P, CH, 4>(e, tw0); break;
+            case 2: r4_dif_w4_grow<P, CH, 8>(e, tw0); break;
+            default: r4_dif_w4_grow<P, CH, 16>(e, tw0); break;
+          }
+        } else {
+          switch (r) {
+            case 0: r4_dif_grow<P, CH, 2>(e, tw0, tw1, tw2); break;
+            case 1: r4_dif_grow<P, CH, 4>(e, tw0, tw1, tw2); break;
+            default: r4_dif_grow<P, CH, 8>(e, tw0, tw1, tw2); break;
+          }
+        }
+      } else if (s == 1) {
+        r4_dif_w4<P, CH>(e, tw0);
+      } else {
+        r4_dif<P, CH>(e, tw0, tw1, tw2);
+      }
     } else {
-      r4_dit<P, CH>(e, ntt_tw(sub, jj << (t - ls - 1)), ntt_tw(sub, jj << (t - ls - 2)), ntt_tw(sub, (jj + s) << (t - ls - 2)));
+      // twiddles loaded where they are used (the DIT pass keeps four waves)
+      const int ls = quarter(r);
+      const int jj = k & (s - 1);
+      if (grow) {
+        if (s == 1) {
+          const Fe<P> w4 = ntt_tw(sub, 1 << (t - 2));
+          switch (r) {
+            case 0: r4_dif_w4_grow<P, CH, 2>(e, w4); break;
+            case 1: r4_dif_w4_grow<P, CH, 4>(e, w4); break;
+            case 2: r4_dif_w4_grow<P, CH, 8>(e, w4); break;
+            default: r4_dif_w4_grow<P, CH, 16>(e, w4); break;
+          }
+        } else {
+          const Fe<P> t1 = ntt_tw(sub, jj << (t - ls - 2)), t2 = ntt_tw(sub, (jj + s) << (t - ls - 2)),
+                      t3 = ntt_tw(sub, jj << (t - ls - 1));
+          switch (r) {
+            case 0: r4_dif_grow<P, CH, 2>(e, t1, t2, t3); break;
+            case 1: r4_dif_grow<P, CH, 4>(e, t1, t2, t3); break;
+            default: r4_dif_grow<P, CH, 8>(e, t1, t2, t3); break;
+          }
+        }
+      } else if (s == 1) {  // block-uniform
+        const Fe<P> w4 = ntt_tw(sub, 1 << (t - 2));
+        if (DIT) r4_dit_w4<P, CH>(e, w4);
+        else r4_dif_w4<P, CH>(e, w4);
+      } else if (!DIT) {
+        r4_dif<P, CH>(e, ntt_tw(sub, jj << (t - ls - 2)), ntt_tw(sub, (jj + s) << (t - ls - 2)),
+                      ntt_tw(sub, jj << (t - ls - 1)));
+      } else {
+        r4_dit<P, CH>(e, ntt_tw(sub, jj << (t - ls - 1)), ntt_tw(sub, jj << (t - ls - 2)),
+                      ntt_tw(sub, (jj + s) << (t - ls - 2)));
+      }
     }
+    if (tw_ahead && r + 1 < nr) r4_fetch_tw<P, DIT>(sub, t, quarter(r + 1), k, tw0, tw1, tw2);
   }
   if (t & 1) {
     // the lone radix-2 stage on the tile (DIF lm = 0 after the rounds: inputs
@@ -477,9 +591,9 @@ __global__ void __launch_bounds__(NTT_TPB) __attribute__((amdgpu_waves_per_eu(NT
     Fe<P> v = e[I];
     if (!DIT && lo > 0) {
       // inter-pass twiddle of a DIF pass (never the last pass): stored < 2p
-      v = fe_mul_lz(v, ld_tab(tw, ((size_t)j << lo) + (o & lomask)));
+      v = fe_mul<P, false, CH>(v, ld_tab(tw, ((size_t)j << lo) + (o & lomask)));
     } else if (post) {
-      v = fe_mul(v, ld_tab(post, addr));  // inputs < 8p: (8p) p < R' p, output canonical
+      v = fe_mul<P, true, CH>(v, ld_tab(post, addr));  // inputs < 8p: (8p) p < R' p, output canonical
     } else if (DIT && !last_pass) {
       // lazily reduced (< 4p < 2^256): the next DIT pass multiplies it on load
     } else {
@@ -808,8 +922,11 @@ static int run_passes(gm_ctx* ctx, NttDomain<C>* d, Fe<typename C::Fr>* a, bool 
   static const bool swg = getenv("GM_NTT_SWG") ? atoi(getenv("GM_NTT_SWG")) != 0 : true;
   // radix-4 passes (k_ntt_pass4) by default; GM_NTT_R4=0: the radix-2 kernel (A/B)
   static const bool r4 = getenv("GM_NTT_R4") ? atoi(getenv("GM_NTT_R4")) != 0 : true;
-  // GM_NTT_CHAIN=1: one dependent mad chain per product (fe_mul CHAIN; A/B)
-  static const bool r4chain = getenv("GM_NTT_CHAIN") ? atoi(getenv("GM_NTT_CHAIN")) != 0 : false;
+  // one dependent mad chain per product (fe_mul CHAIN: the compiler otherwise sums
+  // each column in two halves and adds them, v_lshl_add_u64 per column; 2.20-2.23
+  // -> 2.10-2.12 ms per 2^24 transform, profiles/r04h_ntt_ab.txt); GM_NTT_CHAIN=0: A/B
+  static const bool r4chain = getenv("GM_NTT_CHAIN") ? atoi(getenv("GM_NTT_CHAIN")) != 0 : true;
+  static const bool r4grow = getenv("GM_NTT_GROW") ? atoi(getenv("GM_NTT_GROW")) != 0 : true;
   const size_t smem = sizeof(Fe<Fr>) * (NTT_TILE + (swg ? 0 : (1 << (NTT_TMAX - 1))));
   const int np = (int)d->passes.size();
   for (int k = 0; k < np; k++) {
@@ -827,7 +944,7 @@ static int run_passes(gm_ctx* ctx, NttDomain<C>* d, Fe<typename C::Fr>* a, bool 
       auto k4 = dit ? (r4chain ? k_ntt_pass4<Fr, true, true> : k_ntt_pass4<Fr, true>)
                     : (r4chain ? k_ntt_pass4<Fr, false, true> : k_ntt_pass4<Fr, false>);
       hipLaunchKernelGGL(k4, dim3(grid), dim3(NTT_TPB),
-                         sizeof(Fe<Fr>) * NTT_TILE, st, a, d->logn, ps.lo, ps.t, tw, sub, first ? fz.pre : nullptr,
+                         sizeof(Fe<Fr>) * NTT_TILE, st, a, d->logn, ps.lo, ps.t, r4grow, tw, sub, first ? fz.pre : nullptr,
                          last ? fz.post : nullptr, first ? fz.pb : nullptr, first ? fz.pc : nullptr);
       continue;
     }
