@@ -298,6 +298,14 @@ def secondary(ctx, gm, args):
     res["ntt"] = {"logn": args.ntt_logn, "gelem_per_s": round(nn / dt / 1e9, 4), "ms_per_transform": round(dt * 1e3, 4),
                   "achieved_gbs": round(gbs, 1), "frac_hbm": round(gbs / HBM_PEAK_GBS, 4),
                   "avg_pass_ms": round(avg_pass, 4), "passes_per_transform": round(pass_cnt / (2 * reps), 2)}
+    # the butterflies' products priced at the mad-only issue peak (every radix-2
+    # butterfly multiplies once, w^0 included: 162 v_mad_u64_u32 for 9 limbs;
+    # inter-pass twiddles, coset / 1/n factors and reductions not counted)
+    bfly_mads = args.ntt_logn * (nn // 2) * 2 * 81
+    tm = bfly_mads / dt / 1e12
+    res["ntt"]["int_alu"] = {"achieved": round(tm, 3), "peak": round(MAD_PEAK_T, 2), "unit": "T v_mad_u64_u32/s",
+                             "frac": round(tm / MAD_PEAK_T, 4),
+                             "work": "%d stages x %d butterflies x 162 mads" % (args.ntt_logn, nn // 2)}
     if not args.no_cpu_baseline:
         res["ntt"]["cpu_baseline"] = ntt_cpu_baseline(ctx, min(args.ntt_logn, 22))
     if args.msm_extra:

@@ -341,13 +341,6 @@ struct gm_msm_pending {
 };
 
 namespace {
-// ctx->stream temporarily replaced (all MSM code queues on ctx->stream)
-struct StreamSwap {
-  gm_ctx* ctx;
-  hipStream_t old;
-  StreamSwap(gm_ctx* c, hipStream_t s) : ctx(c), old(c->stream) { c->stream = s; }
-  ~StreamSwap() { ctx->stream = old; }
-};
 template <class C, bool G2>
 int msm_wait_t(gm_msm_pending* p, void* out_jac, void* out_aff) {
   using HF = typename GroupSel<C, G2>::HF;

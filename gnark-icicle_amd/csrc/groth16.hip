@@ -850,29 +850,60 @@ int g16_sums_t(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, HSource& hs, G
   // and Horner, msm_finish) overlaps the device work of the next, each MSM in
   // one of the context's two slot arenas.  The G1 and G2 B-MSMs
   // (prove.go:217,293) share scalars and layout: one plan, in slot 1.
+  // Slot 1's MSMs (B, B2, Z) queue on a second stream (GM_G16_MSM_STREAMS=1),
+  // ordered after the plans / gathers: one MSM's bucket reduction (latency-bound,
+  // one or two waves per SIMD) then runs beside the next one's accumulation
+  // instead of before it.
+  static const bool two = getenv("GM_G16_MSM_STREAMS") && atoi(getenv("GM_G16_MSM_STREAMS")) != 0;
+  hipStream_t st1 = st;
+  if (two) {
+    if (!ctx->slot_stream[1]) GM_HIP(hipStreamCreateWithFlags(&ctx->slot_stream[1], hipStreamNonBlocking));
+    st1 = ctx->slot_stream[1];
+    hipEvent_t ev;
+    GM_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    const hipError_t e1 = hipEventRecord(ev, st);  // the gathers and the shared plan
+    const hipError_t e2 = e1 == hipSuccess ? hipStreamWaitEvent(st1, ev, 0) : e1;
+    hipEventDestroy(ev);
+    GM_HIP(e2);
+  }
   SlotArena s0(ctx), s1(ctx);
   MsmTail tA, tB, tB2, tK, tZ;
   if ((rc = hs.poll()) || (rc = s0.take())) return rc;
   if ((rc = launch_x(0, *s0.a, pk->A, tA))) return rc;
   if ((rc = hs.poll()) || (rc = s1.take())) return rc;
-  if (!have[1]) {
-    if ((rc = msm_plan<C>(ctx, *s1.a, wX[1].p, pk->nbB, pB, planX[1]))) return rc;
+  {
+    StreamSwap sw(ctx, st1);
+    if (!have[1]) {
+      if ((rc = msm_plan<C>(ctx, *s1.a, wX[1].p, pk->nbB, pB, planX[1]))) return rc;
+    }
+    if ((rc = msm_launch<C, false>(ctx, *s1.a, planX[1], pk->B, tB))) return rc;
   }
-  if ((rc = msm_launch<C, false>(ctx, *s1.a, planX[1], pk->B, tB))) return rc;
   if ((rc = msm_finish<C, false>(ctx, tA, out.A))) return rc;
   s0.release();
-  if ((rc = hs.poll()) || (rc = msm_launch<C, true>(ctx, *s1.a, planX[1], pk->B2, tB2))) return rc;
-  if ((rc = msm_finish<C, false>(ctx, tB, out.B))) return rc;
+  if ((rc = hs.poll())) return rc;
+  {
+    StreamSwap sw(ctx, st1);
+    if ((rc = msm_launch<C, true>(ctx, *s1.a, planX[1], pk->B2, tB2)) ||
+        (rc = msm_finish<C, false>(ctx, tB, out.B)))
+      return rc;
+  }
   if (on_ab) on_ab(out);
   if ((rc = hs.poll()) || (rc = s0.take())) return rc;
   if ((rc = launch_x(2, *s0.a, pk->K, tK))) return rc;
-  if ((rc = msm_finish<C, true>(ctx, tB2, out.B2))) return rc;
+  {
+    StreamSwap sw(ctx, st1);
+    if ((rc = msm_finish<C, true>(ctx, tB2, out.B2))) return rc;
+  }
   s1.release();
   const void* zs = nullptr;
-  if ((rc = hs.z_scalars(&zs)) || (rc = s1.take())) return rc;
-  if ((rc = msm_device_launch<C, false>(ctx, *s1.a, zs, pk->Z, pk->nbZ, true, pZ, tZ))) return rc;
+  {
+    StreamSwap sw(ctx, st1);  // Z waits for h on its own stream
+    if ((rc = hs.z_scalars(&zs)) || (rc = s1.take())) return rc;
+    if ((rc = msm_device_launch<C, false>(ctx, *s1.a, zs, pk->Z, pk->nbZ, true, pZ, tZ))) return rc;
+  }
   if ((rc = msm_finish<C, false>(ctx, tK, out.K))) return rc;
   s0.release();
+  StreamSwap sw(ctx, st1);
   return msm_finish<C, false>(ctx, tZ, out.Z);
 }
 

@@ -182,6 +182,16 @@ struct Arena {
 };
 
 // A deferred-tail arena slot of the context (at most two MSMs in flight).
+// ctx->stream temporarily replaced (all MSM code queues on ctx->stream)
+struct StreamSwap {
+  gm_ctx* ctx;
+  hipStream_t old;
+  StreamSwap(gm_ctx* c, hipStream_t s) : ctx(c), old(c->stream) { c->stream = s; }
+  ~StreamSwap() { ctx->stream = old; }
+  StreamSwap(const StreamSwap&) = delete;
+  StreamSwap& operator=(const StreamSwap&) = delete;
+};
+
 struct SlotArena {
   gm_ctx* ctx;
   int k = -1;
