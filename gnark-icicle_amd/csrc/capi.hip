@@ -368,11 +368,13 @@ int gm_msm_async(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const 
   p->curve = curve;
   p->g2 = g2 ? 1 : 0;
   int rc = p->slot.take();
-  // Slot stream, opt-in (GM_MSM_SLOT_STREAMS=1): measured no faster than one
-  // stream for back-to-back 2^20 G1 MSMs (2.31 vs 2.29 ms/step; the
-  // accumulation already fills the chip).  It starts after the work already
-  // queued on ctx->stream (the inputs).
-  static const bool slot_streams = getenv("GM_MSM_SLOT_STREAMS") && !strcmp(getenv("GM_MSM_SLOT_STREAMS"), "1");
+  // One stream per slot (GM_MSM_SLOT_STREAMS=0: everything on ctx->stream).  With
+  // a hardware queue per stream (GPU_MAX_HW_QUEUES >= 8: HIP's default 4 puts both
+  // slot streams on one queue) one MSM's fixup / reduction / readback overlaps the
+  // next one's accumulation: back-to-back 2^20 G1 MSMs 1.95-1.99 -> 1.90-1.92 ms
+  // (profiles/r04m_hwq_ab.txt).  It starts after the work already queued on
+  // ctx->stream (the inputs).
+  static const bool slot_streams = !getenv("GM_MSM_SLOT_STREAMS") || atoi(getenv("GM_MSM_SLOT_STREAMS")) != 0;
   p->st = ctx->stream;
   if (rc == GM_OK && slot_streams) {
     hipStream_t& ss = ctx->slot_stream[p->slot.k];
