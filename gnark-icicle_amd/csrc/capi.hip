@@ -139,7 +139,18 @@ int gm_init(int device, gm_ctx** out) {
   if (const char* sl = getenv("GM_MSM_SLICE")) c->msm_slice = atoi(sl) > 0 ? atoi(sl) : 0;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
+  // the host->device input copies (HostStagedH's helper thread, the staged ring)
+  // must not queue behind kernels: a pageable copy is staged chunk by chunk, each
+  // chunk's DMA waiting on the copy stream's hardware queue.  GM_COPY_STREAM_PRIO=1
+  // gives the copy stream the highest priority (a queue of its own; A/B).
+  static const bool copy_prio = getenv("GM_COPY_STREAM_PRIO") && atoi(getenv("GM_COPY_STREAM_PRIO")) != 0;
+  if (e == hipSuccess) {
+    int lo = 0, hi = 0;
+    if (copy_prio && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
+      e = hipStreamCreateWithPriority(&c->copy, hipStreamNonBlocking, hi);
+    else
+      e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
+  }
   if (e != hipSuccess) {
     set_error(std::string("hipStreamCreate: ") + hipGetErrorString(e));
     delete c;
@@ -176,6 +187,11 @@ int gm_destroy(gm_ctx* ctx) {
   if (ctx->aux) hipStreamDestroy(ctx->aux);
   if (ctx->copy) hipStreamDestroy(ctx->copy);
   if (ctx->pinned) hipHostFree(ctx->pinned);
+  if (ctx->in_abc) hipFree(ctx->in_abc);
+  for (int i = 0; i < gm_ctx::H2D_SLOTS; i++) {
+    if (ctx->h2d_pin[i]) hipHostFree(ctx->h2d_pin[i]);
+    if (ctx->h2d_ev[i]) hipEventDestroy(ctx->h2d_ev[i]);
+  }
   delete ctx;
   return GM_OK;
 }

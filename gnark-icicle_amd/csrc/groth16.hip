@@ -523,14 +523,46 @@ struct HostStagedH : HSource {
   int start() {
     int rc;
     if ((rc = ev.create())) return rc;
+    // GM_G16_H2D_PINNED=0: plain pageable copies (A/B).  A pageable copy issued
+    // from this thread while the MSMs ran could stall until an accumulation kernel
+    // ended (fresh process: copies after the B2 MSM, 2^24 prove 199 ms instead of
+    // ~167, profiles/r04s_g16_host_slow_copies.txt); through the context's pinned
+    // ring (memcpy into a 32 MiB slot, then an async copy from pinned memory) the
+    // DMA does not wait for the kernels.
+    static const bool pinned = !getenv("GM_G16_H2D_PINNED") || atoi(getenv("GM_G16_H2D_PINNED")) != 0;
     th = std::thread([this] {
       int r = GM_OK;
       if (hipSetDevice(ctx->device) != hipSuccess) r = GM_ERR_DEVICE;
       const void* src[3] = {ha, hb, hc};
       void* dst[3] = {da, db, dc};
-      for (int k = 0; k < 3 && r == GM_OK; k++)
-        if (nc && hipMemcpyAsync(dst[k], src[k], 32 * nc, hipMemcpyHostToDevice, ctx->copy) != hipSuccess)
-          r = GM_ERR_DEVICE;
+      if (pinned) {
+        for (int i = 0; i < gm_ctx::H2D_SLOTS && r == GM_OK; i++) {
+          if (!ctx->h2d_pin[i] && hipHostMalloc(&ctx->h2d_pin[i], gm_ctx::H2D_SLOT, hipHostMallocDefault) != hipSuccess)
+            r = GM_ERR_OOM;
+          if (r == GM_OK && !ctx->h2d_ev[i] &&
+              hipEventCreateWithFlags(&ctx->h2d_ev[i], hipEventDisableTiming) != hipSuccess)
+            r = GM_ERR_DEVICE;
+        }
+        bool used[gm_ctx::H2D_SLOTS] = {};
+        int slot = 0;
+        for (int k = 0; k < 3 && r == GM_OK; k++)
+          for (size_t off = 0; off < 32 * nc && r == GM_OK; off += gm_ctx::H2D_SLOT) {
+            const size_t len = std::min(gm_ctx::H2D_SLOT, 32 * nc - off);
+            if (used[slot] && hipEventSynchronize(ctx->h2d_ev[slot]) != hipSuccess) r = GM_ERR_DEVICE;
+            if (r) break;
+            memcpy(ctx->h2d_pin[slot], (const char*)src[k] + off, len);
+            if (hipMemcpyAsync((char*)dst[k] + off, ctx->h2d_pin[slot], len, hipMemcpyHostToDevice, ctx->copy) !=
+                    hipSuccess ||
+                hipEventRecord(ctx->h2d_ev[slot], ctx->copy) != hipSuccess)
+              r = GM_ERR_DEVICE;
+            used[slot] = true;
+            slot = (slot + 1) % gm_ctx::H2D_SLOTS;
+          }
+      } else {
+        for (int k = 0; k < 3 && r == GM_OK; k++)
+          if (nc && hipMemcpyAsync(dst[k], src[k], 32 * nc, hipMemcpyHostToDevice, ctx->copy) != hipSuccess)
+            r = GM_ERR_DEVICE;
+      }
       if (r == GM_OK && hipEventRecord(ev.a, ctx->copy) != hipSuccess) r = GM_ERR_DEVICE;
       if (r) copy_err = "staged a/b/c upload failed";
       copy_rc = r;
@@ -1145,15 +1177,29 @@ int gm_g16_prove(gm_ctx* ctx, gm_g16_pk* pk, const void* wires, const void* a, c
   std::lock_guard<std::recursive_mutex> g(ctx->mu);
   GM_HIP(hipSetDevice(ctx->device));
   Arena arena(ctx);
-  DevBuf w, da, db, dc;
+  DevBuf w;
   int rc;
-  if ((rc = w.alloc(arena, 32 * pk->nb_wires)) || (rc = da.alloc(arena, 32 * pk->n)) ||
-      (rc = db.alloc(arena, 32 * pk->n)) || (rc = dc.alloc(arena, 32 * pk->n)))
-    return rc;
+  if ((rc = w.alloc(arena, 32 * pk->nb_wires))) return rc;
+  // a / b / c: the context's input allocation (gm_ctx::in_abc), not the arena
+  const size_t abc = 3 * 32 * pk->n;
+  if (ctx->in_abc_cap < abc) {
+    if (ctx->in_abc) GM_HIP(hipFree(ctx->in_abc));
+    ctx->in_abc = nullptr;
+    ctx->in_abc_cap = 0;
+    if (hipMalloc(&ctx->in_abc, abc) != hipSuccess) {
+      ctx->in_abc = nullptr;
+      set_error("prove: hipMalloc of the a/b/c input buffer failed");
+      return GM_ERR_OOM;
+    }
+    ctx->in_abc_cap = abc;
+  }
+  char* const da = (char*)ctx->in_abc;
+  char* const db = da + 32 * pk->n;
+  char* const dc = db + 32 * pk->n;
   GM_HIP(hipMemcpyAsync(w.p, wires, 32 * pk->nb_wires, hipMemcpyHostToDevice, ctx->stream));
-  rc = pk->curve == GM_BN254 ? g16_prove_t<CurveBN254>(ctx, pk, w.p, da.p, db.p, dc.p, a, b, c, nc, r, s, ar_out,
+  rc = pk->curve == GM_BN254 ? g16_prove_t<CurveBN254>(ctx, pk, w.p, da, db, dc, a, b, c, nc, r, s, ar_out,
                                                        bs_out, krs_out)
-                             : g16_prove_t<CurveBLS12377>(ctx, pk, w.p, da.p, db.p, dc.p, a, b, c, nc, r, s, ar_out,
+                             : g16_prove_t<CurveBLS12377>(ctx, pk, w.p, da, db, dc, a, b, c, nc, r, s, ar_out,
                                                           bs_out, krs_out);
   prof_collect(ctx);
   return rc;

@@ -80,7 +80,19 @@ struct gm_ctx {
   // one stream per slot (gm_msm_async): two independent MSMs in flight overlap
   // on the device -- one's sort / reduction (HBM / latency-bound) runs beside the
   // other's accumulation (VALU-bound).  Created on first use.
-  hipStream_t slot_stream[2] = {nullptr, nullptr};
+  hipStream_t slot_stream[2] = {nullptr, nullptr};  // a / b / c of a host-input prove (gm_g16_prove): their own allocation, outside
+  // the workspace arena.  The runtime orders a pageable copy into an allocation
+  // after the queued commands that use the same allocation, so copies into an
+  // arena chunk shared with MSM scratch waited for the running MSMs (2^24: the
+  // copies ran after the B2 MSM, +35 ms, profiles/r04s_g16_host_slow_copies.txt).
+  void* in_abc = nullptr;
+  size_t in_abc_cap = 0;
+  // pinned ring the host-input prove's helper thread copies a / b / c through
+  // (HostStagedH): created on first use, kept
+  static constexpr int H2D_SLOTS = 4;
+  static constexpr size_t H2D_SLOT = size_t(32) << 20;
+  void* h2d_pin[H2D_SLOTS] = {};
+  hipEvent_t h2d_ev[H2D_SLOTS] = {};
 };
 
 namespace gm {

@@ -93,7 +93,11 @@ int gm_msm(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const void* 
  * arguments) and returns at once; gm_msm_wait finishes it (host tail: checks
  * and the Horner combination) and frees the handle.  The host tail of one MSM
  * thus overlaps the device work of the next one issued before it.  At most two
- * MSMs may be in flight per context; wait in issue order.  Synchronous calls
+ * MSMs may be in flight per context; wait in issue order.  Each in-flight MSM
+ * runs on a stream of its own (GM_MSM_SLOT_STREAMS=0: the context stream), so
+ * one MSM's reduction overlaps the next one's accumulation when the process has
+ * a hardware queue per stream (GPU_MAX_HW_QUEUES=8 before HIP initialises;
+ * HIP's default 4 serialises them).  Synchronous calls
  * (gm_msm, gm_msm_prepared, gm_ntt, ...) may be made on the same context while
  * async MSMs are pending: each pending MSM keeps its own scratch arena and its
  * own pinned readback buffer until its gm_msm_wait. */
