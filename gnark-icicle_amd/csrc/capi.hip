@@ -139,18 +139,7 @@ int gm_init(int device, gm_ctx** out) {
   if (const char* sl = getenv("GM_MSM_SLICE")) c->msm_slice = atoi(sl) > 0 ? atoi(sl) : 0;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking);
-  // the host->device input copies (HostStagedH's helper thread, the staged ring)
-  // must not queue behind kernels: a pageable copy is staged chunk by chunk, each
-  // chunk's DMA waiting on the copy stream's hardware queue.  GM_COPY_STREAM_PRIO=1
-  // gives the copy stream the highest priority (a queue of its own; A/B).
-  static const bool copy_prio = getenv("GM_COPY_STREAM_PRIO") && atoi(getenv("GM_COPY_STREAM_PRIO")) != 0;
-  if (e == hipSuccess) {
-    int lo = 0, hi = 0;
-    if (copy_prio && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
-      e = hipStreamCreateWithPriority(&c->copy, hipStreamNonBlocking, hi);
-    else
-      e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
-  }
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
   if (e != hipSuccess) {
     set_error(std::string("hipStreamCreate: ") + hipGetErrorString(e));
     delete c;
