@@ -31,6 +31,8 @@ sys.path.insert(0, os.path.join(ROOT, "gnark-icicle_amd"))
 # accumulation (+3-4 %, profiles/r04m_hwq_ab.txt).  Read at HIP initialisation: set
 # before torch is imported.
 os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# MSMs in flight in the step loop (gm_msm_async allows up to 3 per context)
+PIPE_DEPTH = int(os.environ.get("GM_BENCH_PIPE_DEPTH", "3"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (8.0 TB/s spec)
 MSM_BYTES_PER_POINT = 96  # 64 B affine point + 32 B scalar
@@ -140,17 +142,20 @@ def main():
         return gm.reduce_partials("bn254", False, gm.allgather_partial(local))
 
     def run(k):
-        """k MSMs, pipelined two deep (gm_msm_async): step i+1's device work is
-        queued before step i's host tail (readback checks + Horner, and at N > 1
-        the RCCL all-gather of the partials and the host adds) runs, so the tail
-        overlaps the GPU; every result is complete when run returns."""
-        pend, r = None, None
+        """k MSMs, pipelined PIPE_DEPTH deep (gm_msm_async, one stream per MSM):
+        steps i+1 .. i+PIPE_DEPTH-1 are queued before step i's host tail
+        (readback checks + Horner, and at N > 1 the RCCL all-gather of the
+        partials and the host adds) runs, so the tail overlaps the GPU and one
+        MSM's sort / reduction overlaps another's accumulation; every result is
+        complete when run returns."""
+        pend, r = [], None
         for _ in range(k):
-            nxt = ctx.msm_async("bn254", S, P, n)
-            if pend is not None:
-                r = finish(pend)
-            pend = nxt
-        return finish(pend) if pend is not None else r
+            pend.append(ctx.msm_async("bn254", S, P, n))
+            if len(pend) == PIPE_DEPTH:
+                r = finish(pend.pop(0))
+        while pend:
+            r = finish(pend.pop(0))
+        return r
 
     run(args.warmup)
     # unpipelined latency of one MSM (synchronous gm_msm), for reference
@@ -228,9 +233,9 @@ def main():
                    "points_per_gpu": n, "total_points": total_points, "parallelism": "msm-shard%d" % world},
         "roofline": roofline,
         "kernel_avg_ms": kernel_ms,
-        "pipeline": "steps pipelined two deep (gm_msm_async / gm_msm_wait): step i+1's device work is queued "
-                    "before step i's host tail (N > 1: incl. the all-gather of partials and the host adds); "
-                    "latency_ms = one synchronous (N > 1: sharded) MSM",
+        "pipeline": ("steps pipelined %d deep (gm_msm_async / gm_msm_wait, one stream per MSM): the next steps' "
+                     "device work is queued before step i's host tail (N > 1: incl. the all-gather of partials and "
+                     "the host adds); latency_ms = one synchronous (N > 1: sharded) MSM" % PIPE_DEPTH),
         "latency_ms": round(lat_ms, 4),
     }
 

@@ -156,7 +156,7 @@ int gm_destroy(gm_ctx* ctx) {
   if (ctx->aux) hipStreamSynchronize(ctx->aux);
   if (ctx->copy) hipStreamSynchronize(ctx->copy);
   ntt_domains_free(ctx);
-  for (gm::ArenaState* a : {&ctx->arena, &ctx->slots[0], &ctx->slots[1]}) {
+  for (gm::ArenaState* a : {&ctx->arena, &ctx->slots[0], &ctx->slots[1], &ctx->slots[2]}) {
     for (auto& ch : a->chunks) hipFree(ch.base);
     a->chunks.clear();
   }

@@ -69,18 +69,21 @@ struct gm_ctx {
   // workspace arena (stack-discipline scopes), plus two more for MSMs whose host
   // tail is deferred (pipelined MSMs: gm_msm_async, the Groth16 MSM sequence)
   gm::ArenaState arena;
-  gm::ArenaState slots[2];
-  bool slot_busy[2] = {false, false};
+  // MSM_SLOTS in-flight MSMs (gm_msm_async; the Groth16 sequence uses two)
+  static constexpr int MSM_SLOTS = 3;
+  gm::ArenaState slots[MSM_SLOTS];
+  bool slot_busy[MSM_SLOTS] = {};
   // pinned readback buffers of deferred MSM tails; a buffer stays busy from
   // msm_readback until its MSM's msm_finish (or the tail's destruction), so
   // synchronous MSMs issued while async ones are pending never reuse it
   static constexpr int TAIL_BUFS = 8;
   void* tail_pinned[TAIL_BUFS] = {};
   bool tail_busy[TAIL_BUFS] = {};
-  // one stream per slot (gm_msm_async): two independent MSMs in flight overlap
-  // on the device -- one's sort / reduction (HBM / latency-bound) runs beside the
-  // other's accumulation (VALU-bound).  Created on first use.
-  hipStream_t slot_stream[2] = {nullptr, nullptr};  // a / b / c of a host-input prove (gm_g16_prove): their own allocation, outside
+  // one stream per slot (gm_msm_async): independent MSMs in flight overlap on
+  // the device -- one's sort / reduction (HBM / latency-bound) runs beside
+  // another's accumulation (VALU-bound).  Created on first use.
+  hipStream_t slot_stream[MSM_SLOTS] = {};
+  // a / b / c of a host-input prove (gm_g16_prove): their own allocation, outside
   // the workspace arena.  The runtime orders a pageable copy into an allocation
   // after the queued commands that use the same allocation, so copies into an
   // arena chunk shared with MSM scratch waited for the running MSMs (2^24: the
@@ -193,7 +196,7 @@ struct Arena {
   }
 };
 
-// A deferred-tail arena slot of the context (at most two MSMs in flight).
+// A deferred-tail arena slot of the context (at most MSM_SLOTS MSMs in flight).
 // ctx->stream temporarily replaced (all MSM code queues on ctx->stream)
 struct StreamSwap {
   gm_ctx* ctx;
@@ -209,14 +212,14 @@ struct SlotArena {
   int k = -1;
   Arena* a = nullptr;
   int take() {
-    for (int i = 0; i < 2; i++)
+    for (int i = 0; i < gm_ctx::MSM_SLOTS; i++)
       if (!ctx->slot_busy[i]) {
         k = i;
         ctx->slot_busy[i] = true;
         a = new Arena(ctx, &ctx->slots[i]);
         return GM_OK;
       }
-    set_error("at most two MSMs may be in flight per context");
+    set_error("at most " + std::to_string(gm_ctx::MSM_SLOTS) + " MSMs may be in flight per context");
     return GM_ERR_INVALID;
   }
   void release() {

@@ -307,7 +307,7 @@ class Context:
 
     def msm_async(self, curve, scalars: DeviceBuffer, points: DeviceBuffer, n: int, g2: bool = False):
         """Queues an MSM (gm_msm_async); .wait() returns (jacobian_bytes, affine_bytes).
-        At most two in flight per context, waited in issue order."""
+        At most three in flight per context, waited in issue order."""
         h = ctypes.c_void_p()
         sp = scalars.ptr if isinstance(scalars, DeviceBuffer) else scalars
         pp = points.ptr if isinstance(points, DeviceBuffer) else points

@@ -92,7 +92,7 @@ int gm_msm(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const void* 
 /* Pipelined MSM: gm_msm_async queues the device work of gm_msm (same
  * arguments) and returns at once; gm_msm_wait finishes it (host tail: checks
  * and the Horner combination) and frees the handle.  The host tail of one MSM
- * thus overlaps the device work of the next one issued before it.  At most two
+ * thus overlaps the device work of the next one issued before it.  At most three
  * MSMs may be in flight per context; wait in issue order.  Each in-flight MSM
  * runs on a stream of its own (GM_MSM_SLOT_STREAMS=0: the context stream), so
  * one MSM's reduction overlaps the next one's accumulation when the process has

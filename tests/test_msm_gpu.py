@@ -406,8 +406,9 @@ def test_msm_three_level_sort_skewed(gm_ctx, oracle, monkeypatch):
 
 
 def test_msm_async_pipelined(gm_ctx, oracle):
-    """gm_msm_async / gm_msm_wait: two MSMs in flight (different curves, groups
-    and sizes), waited in order, equal the oracle; a third in flight is refused."""
+    """gm_msm_async / gm_msm_wait: MSMs in flight (different curves, groups and
+    sizes), waited in order, equal the oracle; three may be in flight, a fourth
+    is refused."""
     import gnark_mi355x as gm
     cases = []
     for cname, g2, n in (("bn254", False, 5000), ("bls12377", True, 777), ("bn254", True, 3000)):
@@ -424,10 +425,11 @@ def test_msm_async_pipelined(gm_ctx, oracle):
                 assert pend[k - 1].wait()[1] == cases[k - 1][5]
         assert pend[-1].wait()[1] == cases[-1][5]
         a = gm_ctx.msm_async("bn254", cases[0][3], cases[0][4], cases[0][2])
-        b = gm_ctx.msm_async("bn254", cases[0][3], cases[0][4], cases[0][2])
+        b = gm_ctx.msm_async(cases[1][0], cases[1][3], cases[1][4], cases[1][2], cases[1][1])
+        c = gm_ctx.msm_async("bn254", cases[0][3], cases[0][4], cases[0][2])
         with pytest.raises(gm.GmError, match="in flight"):
             gm_ctx.msm_async("bn254", cases[0][3], cases[0][4], cases[0][2])
-        assert a.wait()[1] == cases[0][5] and b.wait()[1] == cases[0][5]
+        assert a.wait()[1] == cases[0][5] and b.wait()[1] == cases[1][5] and c.wait()[1] == cases[0][5]
     finally:
         for c in cases:
             c[3].free()
