@@ -59,8 +59,8 @@ PMC_VALU_FILE = "profiles/r04g_pmc_valu.json"
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--logn", type=int, default=20, help="MSM points per GPU = 2^logn")
     ap.add_argument("--ntt-logn", type=int, default=24)
     ap.add_argument("--g16-logn", type=str, default="20,24", help="Groth16 prove domains, comma list ('' = skip)")
@@ -158,11 +158,17 @@ def main():
         return r
 
     run(args.warmup)
-    # unpipelined latency of one MSM (synchronous gm_msm), for reference
+    # unpipelined latency of one MSM (synchronous gm_msm), for reference; its
+    # kernel timings give the accumulation's launch time with nothing beside it
+    ctx.profile_reset()
+    ctx.profile(True)
     t0 = time.perf_counter()
     for _ in range(3):
         step()
     lat_ms = (time.perf_counter() - t0) / 3 * 1e3
+    ctx.profile(False)
+    iso_ms, iso_cnt = ctx.profile_stats().get("msm_accum_g1", (0.0, 0))
+    iso_avg_ms = iso_ms / max(iso_cnt, 1)
     ctx.profile_reset()
     ctx.profile(True)
     barrier()
@@ -207,6 +213,14 @@ def main():
                     "frac": round(tmads / MAD_PEAK_T, 4),
                     "work": "%d %spoints x %d windows XYZZ mixed adds x %d mads" % (
                         npts, "GLV (P, phi(P)) " if glv else "", windows, MADS_PER_MIXED_ADD)},
+        # the timed steps overlap MSMs (slot streams), so avg_launch_ms above includes
+        # the time the accumulation shares the chip with its neighbours' sorts and
+        # reductions; the same kernel alone (the synchronous latency MSMs):
+        "isolated": ({"avg_launch_ms": round(iso_avg_ms, 4),
+                      "achieved": round(alg_bytes / (iso_avg_ms * 1e-3) / 1e9, 2),
+                      "frac": round(alg_bytes / (iso_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                      "int_alu_frac": round(mads / (iso_avg_ms * 1e-3) / 1e12 / MAD_PEAK_T, 4)}
+                     if iso_avg_ms > 0 else None),
         "valu": load_pmc_valu("k_msm_accum_seg<Fe<Bn254Fp> >"),
         "valu_source": PMC_VALU_FILE + " (rocprofv3 --pmc SQ_* passes; committed profile, not measured in this run)",
         "note": "bound=hbm is the bench contract's roofline for this non-MFMA path; the kernel is NOT HBM-bound: "
