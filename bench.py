@@ -24,10 +24,10 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "gnark-icicle_amd"))
-# The two MSMs the step loop keeps in flight run on their own streams (gm_msm_async
+# The MSMs the step loop keeps in flight run on their own streams (gm_msm_async
 # slot streams); HIP's default of 4 hardware queues is shared by torch's stream and the
-# context's main / aux / copy streams, so both slot streams would land on one queue and
-# run back to back.  8 queues let one MSM's reduction overlap the next one's
+# context's main / aux / copy streams, so the slot streams would share queues and run
+# back to back.  8 queues let one MSM's reduction overlap the next one's
 # accumulation (+3-4 %, profiles/r04m_hwq_ab.txt).  Read at HIP initialisation: set
 # before torch is imported.
 os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
