@@ -109,7 +109,18 @@ def main():
         # visible GPUs) only to rehearse the N>1 code path on a one-GPU box
         local_rank = local_rank % max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(local_rank)
-        dist.init_process_group(os.environ.get("GM_BENCH_BACKEND", "nccl"))
+        # the bench's stdout is its one JSON line: whatever the backend prints while the
+        # group forms (gloo's "connected to N peer ranks") goes to stderr
+        sys.stdout.flush()
+        saved_stdout = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group(os.environ.get("GM_BENCH_BACKEND", "nccl"))
+            dist.barrier()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved_stdout, 1)
+            os.close(saved_stdout)
     import gnark_mi355x as gm
 
     ctx = gm.Context(local_rank)
