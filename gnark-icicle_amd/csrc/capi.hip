@@ -155,6 +155,8 @@ int gm_destroy(gm_ctx* ctx) {
   hipStreamSynchronize(ctx->stream);
   if (ctx->aux) hipStreamSynchronize(ctx->aux);
   if (ctx->copy) hipStreamSynchronize(ctx->copy);
+  for (hipStream_t s : ctx->slot_stream)
+    if (s) hipStreamSynchronize(s);
   ntt_domains_free(ctx);
   for (gm::ArenaState* a : {&ctx->arena, &ctx->slots[0], &ctx->slots[1], &ctx->slots[2]}) {
     for (auto& ch : a->chunks) hipFree(ch.base);
@@ -168,10 +170,7 @@ int gm_destroy(gm_ctx* ctx) {
     hipEventDestroy(p.b);
   }
   for (hipStream_t s : ctx->slot_stream)
-    if (s) {
-      hipStreamSynchronize(s);
-      hipStreamDestroy(s);
-    }
+    if (s) hipStreamDestroy(s);
   hipStreamDestroy(ctx->stream);
   if (ctx->aux) hipStreamDestroy(ctx->aux);
   if (ctx->copy) hipStreamDestroy(ctx->copy);
