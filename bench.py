@@ -124,6 +124,8 @@ def main():
     import gnark_mi355x as gm
 
     ctx = gm.Context(local_rank)
+    if os.environ.get("GM_BENCH_MSM_WINDOW"):  # window-size sweeps (0 = the cost model)
+        ctx.set_msm_window(int(os.environ["GM_BENCH_MSM_WINDOW"]))
     n = 1 << args.logn
     # ---- resident synthetic inputs: this rank's shard of the MSM ----------------
     seed = 0x5EED0002 + rank
