@@ -1109,7 +1109,14 @@ int msm_launch(gm_ctx* ctx, Arena& arena, const MsmPlan& plan, const void* point
   if (segl_env > 0) Lwant = (uint32_t)segl_env;
   t.L = t.nb >= Lwant ? Lwant : t.nb;
   t.nseg = t.nb / t.L;
-  t.K = ctx->msm_slice ? (uint32_t)ctx->msm_slice : 64u;
+  // Entries per accumulation thread.  64 by default; 32 for G1 MSMs of at most
+  // 2^25 entries (the 2^20 GLV bench MSM: 2^24 entries = 4,096 waves at 64, one
+  // round of four waves per SIMD, so the slowest waves set the time; at 32 the
+  // accumulation alone drops 1.38-1.43 -> 1.34 ms and the pipelined MSM loop gains
+  // 4-7 %, profiles/r04ae_slice_sweep.txt).  Larger MSMs keep 64 (Groth16 2^24:
+  // 156.9 vs 159.3 ms at 32).  The long-span bound FIX_SERIAL * K stays above the
+  // fullest uniform bucket (64 entries at 2^20).  GM_MSM_SLICE overrides.
+  t.K = ctx->msm_slice ? (uint32_t)ctx->msm_slice : (!G2 && plan.M <= (size_t(1) << 25) ? 32u : 64u);
   int rc;
   constexpr int WORDS = Coord<DF>::WORDS;  // u32 words of one gnark-layout coordinate
   static_assert(sizeof(HF) == 4 * WORDS, "host/device layout mismatch");
