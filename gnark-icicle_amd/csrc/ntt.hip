@@ -292,6 +292,11 @@ __global__ void __launch_bounds__(TPB) k_ntt_pass(Fe<P>* __restrict__ data, int 
 #ifndef NTT_TW_PF
 #define NTT_TW_PF 1
 #endif
+// the BN254 DIT kernel: four waves per SIMD (the growing-bound rounds take it from
+// 123 to 132 VGPRs uncapped; capped at 128 it does not spill)
+#ifndef NTT_DIT_WPE_BN254
+#define NTT_DIT_WPE_BN254 4
+#endif
 // the DIF kernel (inter-pass twiddles on the store) separately: -DNTT_DIF_WPE=3
 #ifndef NTT_DIF_WPE
 #define NTT_DIF_WPE NTT_R4_WPE
@@ -408,6 +413,36 @@ GM_DEV void r4_dit_w4(Fe<P> (&e)[4], const Fe<P>& w4) {
   e[3] = fe_sub_lz<2>(s1, y);                                    // < 6p
   unroll4([&](auto I) { fe_reduce_k<4>(e[I]); });               // < 4p
 }
+// DIT rounds with growing bounds (even t, GM_NTT_GROW bit 1): no conditional
+// subtraction inside the pass.  The w_4 round takes inputs < 2p and leaves
+// < 8p; a generic round takes < B p and leaves < (B + 4) p (products < 2p, every
+// product input below 19p); the store brings the < 20p (t = 8) outputs below 4p
+// with three subtractions per element instead of four per round.
+template <class P, bool CH>
+GM_DEV void r4_dit_grow(Fe<P> (&e)[4], const Fe<P>& a, const Fe<P>& b, const Fe<P>& c) {
+  const Fe<P> v1 = MUL(e[1], a);                                 // < 2p
+  const Fe<P> v3 = MUL(e[3], a);
+  const Fe<P> s0 = fe_add_lz(e[0], v1);                          // < (B + 2) p
+  const Fe<P> s1 = fe_sub_lz<2>(e[0], v1);
+  const Fe<P> s2 = fe_add_lz(e[2], v3);
+  const Fe<P> y = MUL(fe_sub_cf<3>(e[2], v3), c);                // < 2p
+  const Fe<P> x = MUL(s2, b);
+  e[0] = fe_add_lz(s0, x);                                       // < (B + 4) p
+  e[2] = fe_sub_lz<2>(s0, x);
+  e[1] = fe_add_lz(s1, y);
+  e[3] = fe_sub_lz<2>(s1, y);
+}
+template <class P, bool CH>
+GM_DEV void r4_dit_w4_grow(Fe<P> (&e)[4], const Fe<P>& w4) {
+  const Fe<P> s0 = fe_add_lz(e[0], e[1]);                        // < 4p
+  const Fe<P> s1 = fe_sub_lz<2>(e[0], e[1]);                     // < 4p
+  const Fe<P> s2 = fe_add_lz(e[2], e[3]);                        // < 4p
+  const Fe<P> y = MUL(fe_sub_cf<3>(e[2], e[3]), w4);             // < 2p
+  e[0] = fe_add_lz(s0, s2);                                      // < 8p
+  e[2] = fe_sub_lz<4>(s0, s2);                                   // < 8p
+  e[1] = fe_add_lz(s1, y);                                       // < 6p
+  e[3] = fe_sub_lz<2>(s1, y);                                    // < 6p
+}
 
 #undef MUL
 
@@ -430,7 +465,7 @@ GM_DEV void r4_fetch_tw(const Fe<P>* __restrict__ sub, int t, int ls, int k, Fe<
 }
 
 template <class P, bool DIT, bool CH = false>
-__global__ void __launch_bounds__(NTT_TPB) __attribute__((amdgpu_waves_per_eu(DIT ? NTT_R4_WPE : NTT_DIF_WPE))) k_ntt_pass4(Fe<P>* __restrict__ data, int logn, int lo, int t, bool ntt_grow,
+__global__ void __launch_bounds__(NTT_TPB) __attribute__((amdgpu_waves_per_eu(DIT ? (std::is_same<P, Bn254Fr>::value ? NTT_DIT_WPE_BN254 : NTT_R4_WPE) : NTT_DIF_WPE))) k_ntt_pass4(Fe<P>* __restrict__ data, int logn, int lo, int t, int grow_mask,
                                                        const Fe<P>* __restrict__ tw,
                                                        const Fe<P>* __restrict__ sub,
                                                        const Fe<P>* __restrict__ pre,
@@ -453,7 +488,8 @@ __global__ void __launch_bounds__(NTT_TPB) __attribute__((amdgpu_waves_per_eu(DI
   // growing DIF bounds (r4_dif_grow): passes whose store multiplies every element
   // by an inter-pass twiddle, with no lone radix-2 stage (it takes inputs < 2p);
   // GM_NTT_GROW=0 keeps every round's outputs < 2p (A/B)
-  const bool grow = !DIT && lo > 0 && !(t & 1) && ntt_grow;
+  const bool grow = !DIT && lo > 0 && !(t & 1) && (grow_mask & 1);
+  const bool dgrow = DIT && !(t & 1) && (grow_mask & 2);  // r4_dit_grow
   // rounds: DIF stages (t-1, t-2), (t-3, t-4), ...; DIT (0, 1), (2, 3), ...
   const int nr = t >> 1;
   auto quarter = [&](int r) { return DIT ? 2 * r : t - 2 - 2 * r; };  // ls of round r
@@ -537,11 +573,18 @@ __global__ void __launch_bounds__(NTT_TPB) __attribute__((amdgpu_waves_per_eu(DI
         }
       } else if (s == 1) {  // block-uniform
         const Fe<P> w4 = ntt_tw(sub, 1 << (t - 2));
-        if (DIT) r4_dit_w4<P, CH>(e, w4);
-        else r4_dif_w4<P, CH>(e, w4);
+        if (DIT) {
+          if (dgrow) r4_dit_w4_grow<P, CH>(e, w4);
+          else r4_dit_w4<P, CH>(e, w4);
+        } else {
+          r4_dif_w4<P, CH>(e, w4);
+        }
       } else if (!DIT) {
         r4_dif<P, CH>(e, ntt_tw(sub, jj << (t - ls - 2)), ntt_tw(sub, (jj + s) << (t - ls - 2)),
                       ntt_tw(sub, jj << (t - ls - 1)));
+      } else if (dgrow) {
+        r4_dit_grow<P, CH>(e, ntt_tw(sub, jj << (t - ls - 1)), ntt_tw(sub, jj << (t - ls - 2)),
+                           ntt_tw(sub, (jj + s) << (t - ls - 2)));
       } else {
         r4_dit<P, CH>(e, ntt_tw(sub, jj << (t - ls - 1)), ntt_tw(sub, jj << (t - ls - 2)),
                       ntt_tw(sub, (jj + s) << (t - ls - 2)));
@@ -589,11 +632,16 @@ __global__ void __launch_bounds__(NTT_TPB) __attribute__((amdgpu_waves_per_eu(DI
     const int j = j0 + I * s;
     const size_t addr = base + ((size_t)j << lo);
     Fe<P> v = e[I];
+    if (dgrow && !post) {  // < 20p -> < 4p, the bound the branches below take
+      fe_reduce_k<16>(v);
+      fe_reduce_k<8>(v);
+      fe_reduce_k<4>(v);
+    }
     if (!DIT && lo > 0) {
       // inter-pass twiddle of a DIF pass (never the last pass): stored < 2p
       v = fe_mul<P, false, CH>(v, ld_tab(tw, ((size_t)j << lo) + (o & lomask)));
     } else if (post) {
-      v = fe_mul<P, true, CH>(v, ld_tab(post, addr));  // inputs < 8p: (8p) p < R' p, output canonical
+      v = fe_mul<P, true, CH>(v, ld_tab(post, addr));  // inputs < 20p: (20p) p < R' p, output canonical
     } else if (DIT && !last_pass) {
       // lazily reduced (< 4p < 2^256): the next DIT pass multiplies it on load
     } else {
@@ -926,7 +974,8 @@ static int run_passes(gm_ctx* ctx, NttDomain<C>* d, Fe<typename C::Fr>* a, bool 
   // each column in two halves and adds them, v_lshl_add_u64 per column; 2.20-2.23
   // -> 2.10-2.12 ms per 2^24 transform, profiles/r04h_ntt_ab.txt); GM_NTT_CHAIN=0: A/B
   static const bool r4chain = getenv("GM_NTT_CHAIN") ? atoi(getenv("GM_NTT_CHAIN")) != 0 : true;
-  static const bool r4grow = getenv("GM_NTT_GROW") ? atoi(getenv("GM_NTT_GROW")) != 0 : true;
+  // growing bounds: bit 0 DIF passes (r4_dif_grow), bit 1 DIT passes (r4_dit_grow)
+  static const int r4grow = getenv("GM_NTT_GROW") ? atoi(getenv("GM_NTT_GROW")) : 3;
   const size_t smem = sizeof(Fe<Fr>) * (NTT_TILE + (swg ? 0 : (1 << (NTT_TMAX - 1))));
   const int np = (int)d->passes.size();
   for (int k = 0; k < np; k++) {
