@@ -24,13 +24,6 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "gnark-icicle_amd"))
-# The MSMs the step loop keeps in flight run on their own streams (gm_msm_async
-# slot streams); HIP's default of 4 hardware queues is shared by torch's stream and the
-# context's main / aux / copy streams, so the slot streams would share queues and run
-# back to back.  8 queues let one MSM's reduction overlap the next one's
-# accumulation (+3-4 %, profiles/r04m_hwq_ab.txt).  Read at HIP initialisation: set
-# before torch is imported.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 # MSMs in flight in the step loop (gm_msm_async allows up to 3 per context)
 PIPE_DEPTH = int(os.environ.get("GM_BENCH_PIPE_DEPTH", "3"))
 
@@ -101,7 +94,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # torch first (its import does not initialise HIP, and its HIP runtime must be
+    # the process's first), then the library, before anything initialises HIP: the
+    # library's load-time constructor gives the process 8 hardware queues unless
+    # GPU_MAX_HW_QUEUES is already set (csrc/capi.hip), so the in-flight MSMs'
+    # streams overlap -- the bench sets nothing itself, exactly as a gnark process
+    # calling the Go hook.
     import torch
+    import gnark_mi355x as gm
+    hwq_preset = os.environ.get("GPU_MAX_HW_QUEUES")
+    gm.load_library()
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -121,7 +123,6 @@ def main():
             sys.stdout.flush()
             os.dup2(saved_stdout, 1)
             os.close(saved_stdout)
-    import gnark_mi355x as gm
 
     ctx = gm.Context(local_rank)
     if os.environ.get("GM_BENCH_MSM_WINDOW"):  # window-size sweeps (0 = the cost model)
@@ -264,6 +265,8 @@ def main():
                      "device work is queued before step i's host tail (N > 1: incl. the all-gather of partials and "
                      "the host adds); latency_ms = one synchronous (N > 1: sharded) MSM" % PIPE_DEPTH),
         "latency_ms": round(lat_ms, 4),
+        "hip_hw_queues": {"value": _process_env("GPU_MAX_HW_QUEUES"),
+                          "set_by": "environment" if hwq_preset else "libgnark_mi355x.so load-time default"},
     }
 
     if rank == 0 and not args.no_secondary and world == 1:
@@ -292,6 +295,15 @@ def main():
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def _process_env(name):
+    """The C environment's value (os.environ does not see a library's setenv)."""
+    import ctypes
+    libc = ctypes.CDLL(None)
+    libc.getenv.restype = ctypes.c_char_p
+    v = libc.getenv(name.encode())
+    return v.decode() if v else None
 
 
 R_BN254 = 21888242871839275222246405745257275088548364400416034343698204186575808495617

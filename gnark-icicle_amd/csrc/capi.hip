@@ -1,6 +1,7 @@
 // C-ABI implementation (include/gnark_mi355x.h): context, memory, MSM, KZG,
 // NTT / computeH, host group helpers and synthetic inputs.  The Groth16 prover
 // entry points live in groth16.hip.
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <thread>
@@ -11,6 +12,17 @@
 #include "msm.hpp"
 #include "ntt.hpp"
 #include "runtime.hpp"
+
+// Hardware queues: every in-flight MSM (gm_msm_async) runs on a stream of its own,
+// and with HIP's default of 4 hardware queues per process those streams share a
+// queue with the context's main / aux / copy streams and run back to back.  HIP
+// reads GPU_MAX_HW_QUEUES when its runtime initialises (the first HIP call), so
+// the library raises the default to 8 while it is being loaded -- only when the
+// variable is unset, so a process (or gnark's Go host) that chose a value keeps it.
+// Back-to-back 2^20 G1 MSMs: 503-520 -> 530-554 Mpoints/s (profiles/r04m_hwq_ab.txt).
+__attribute__((constructor)) static void gm_default_hw_queues() {
+  if (!getenv("GPU_MAX_HW_QUEUES")) setenv("GPU_MAX_HW_QUEUES", "8", 0);
+}
 
 namespace gm {
 
@@ -109,6 +121,8 @@ static int check_curve(int curve) {
 
 size_t fp_bytes(int curve) { return curve == GM_BN254 ? 32 : 48; }
 
+void orphan_pending_msms(gm_ctx* ctx);  // below gm_msm_pending
+
 }  // namespace gm
 
 using namespace gm;
@@ -157,6 +171,7 @@ int gm_destroy(gm_ctx* ctx) {
   if (ctx->copy) hipStreamSynchronize(ctx->copy);
   for (hipStream_t s : ctx->slot_stream)
     if (s) hipStreamSynchronize(s);
+  orphan_pending_msms(ctx);
   ntt_domains_free(ctx);
   for (gm::ArenaState* a : {&ctx->arena, &ctx->slots[0], &ctx->slots[1], &ctx->slots[2]}) {
     for (auto& ch : a->chunks) hipFree(ch.base);
@@ -336,13 +351,25 @@ void gm::MsmTail::release_stage() {
 }
 
 struct gm_msm_pending {
-  gm_ctx* ctx;
+  gm_ctx* ctx;  // nullptr once gm_destroy orphaned the handle
   int curve, g2;
   hipStream_t st = nullptr;  // stream the MSM runs on (slot stream or ctx->stream)
   gm::SlotArena slot;
   gm::MsmTail tail;
   explicit gm_msm_pending(gm_ctx* c) : ctx(c), slot(c) {}
 };
+
+// gm_destroy with MSMs pending (its streams already synchronised): every pending
+// handle gives its slot arena and pinned readback buffer back to the context and
+// is marked orphaned; the caller's later gm_msm_wait reports it and frees it.
+void gm::orphan_pending_msms(gm_ctx* ctx) {
+  for (gm_msm_pending* p : ctx->live_msms) {
+    p->tail.release_stage();
+    p->slot.release();
+    p->ctx = nullptr;
+  }
+  ctx->live_msms.clear();
+}
 
 namespace {
 template <class C, bool G2>
@@ -379,6 +406,8 @@ int gm_msm_async(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const 
   // (profiles/r04m_hwq_ab.txt).  It starts after the work already queued on
   // ctx->stream (the inputs).
   static const bool slot_streams = !getenv("GM_MSM_SLOT_STREAMS") || atoi(getenv("GM_MSM_SLOT_STREAMS")) != 0;
+  const hipStream_t main_st = ctx->stream;
+  hipEvent_t inputs_read = nullptr;
   p->st = ctx->stream;
   if (rc == GM_OK && slot_streams) {
     hipStream_t& ss = ctx->slot_stream[p->slot.k];
@@ -389,21 +418,38 @@ int gm_msm_async(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const 
     GM_HIP(hipStreamWaitEvent(ss, ev, 0));
     GM_HIP(hipEventDestroy(ev));
     p->st = ss;
+    // work queued later on ctx->stream (synchronous calls that may overwrite the
+    // scalars or points in place) waits until this MSM has read them: the event is
+    // recorded after the digits and the point conversion, before the accumulation
+    GM_HIP(hipEventCreateWithFlags(&inputs_read, hipEventDisableTiming));
   }
-  StreamSwap sw(ctx, p->st);
-  if (rc == GM_OK) {
-    Arena& a = *p->slot.a;
-    if (curve == GM_BN254)
-      rc = g2 ? msm_device_launch<CurveBN254, true>(ctx, a, scalars_dev, points_dev, n, false, nullptr, p->tail)
-              : msm_device_launch<CurveBN254, false>(ctx, a, scalars_dev, points_dev, n, false, nullptr, p->tail);
-    else
-      rc = g2 ? msm_device_launch<CurveBLS12377, true>(ctx, a, scalars_dev, points_dev, n, false, nullptr, p->tail)
-              : msm_device_launch<CurveBLS12377, false>(ctx, a, scalars_dev, points_dev, n, false, nullptr, p->tail);
+  {
+    StreamSwap sw(ctx, p->st);
+    if (rc == GM_OK) {
+      Arena& a = *p->slot.a;
+      const void* sc = scalars_dev;
+      const void* pt = points_dev;
+      if (curve == GM_BN254)
+        rc = g2 ? msm_device_launch<CurveBN254, true>(ctx, a, sc, pt, n, false, nullptr, p->tail, inputs_read)
+                : msm_device_launch<CurveBN254, false>(ctx, a, sc, pt, n, false, nullptr, p->tail, inputs_read);
+      else
+        rc = g2 ? msm_device_launch<CurveBLS12377, true>(ctx, a, sc, pt, n, false, nullptr, p->tail, inputs_read)
+                : msm_device_launch<CurveBLS12377, false>(ctx, a, sc, pt, n, false, nullptr, p->tail, inputs_read);
+    }
+  }
+  if (inputs_read) {
+    hipError_t e = rc == GM_OK ? hipStreamWaitEvent(main_st, inputs_read, 0) : hipSuccess;
+    hipEventDestroy(inputs_read);
+    if (e != hipSuccess) {
+      set_error(std::string("gm_msm_async: hipStreamWaitEvent: ") + hipGetErrorString(e));
+      rc = GM_ERR_DEVICE;
+    }
   }
   if (rc) {
     delete p;
     return rc;
   }
+  ctx->live_msms.push_back(p);
   *out = p;
   return GM_OK;
 }
@@ -411,7 +457,14 @@ int gm_msm_async(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const 
 int gm_msm_wait(gm_msm_pending* p, void* out_jac, void* out_affine) {
   if (!p) return GM_ERR_INVALID;
   gm_ctx* ctx = p->ctx;
+  if (!ctx) {
+    delete p;
+    set_error("gm_msm_wait: the context was destroyed while this MSM was pending");
+    return GM_ERR_INVALID;
+  }
   std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  auto& live = ctx->live_msms;
+  live.erase(std::remove(live.begin(), live.end(), p), live.end());
   GM_HIP(hipSetDevice(ctx->device));
   int rc;
   StreamSwap sw(ctx, p->st);  // a long-span redo runs on the MSM's own stream

@@ -33,6 +33,17 @@ using namespace gm;
 
 namespace gm {
 
+// A copy between the buffers of two gm_multi devices takes the peer path
+// (hipMemcpyPeerAsync over xGMI) when the devices differ.  GM_MULTI_FORCE_PEER=1
+// (test knob, read per call) takes it for equal devices too, so a one-GPU box
+// runs the peer branches of the multi-device prover (hipMemcpyPeerAsync with
+// equal devices is a plain device-to-device copy).
+static bool cross_device(int a, int b) {
+  if (a != b) return true;
+  const char* f = getenv("GM_MULTI_FORCE_PEER");
+  return f && atoi(f) != 0;
+}
+
 int check_curve_id(int curve) {
   if (curve != GM_BN254 && curve != GM_BLS12_377) {
     set_error("unknown curve id");
@@ -716,7 +727,7 @@ struct ChainRemoteH : RemoteH {
         for (auto& j : jobs) {
           int r = compute_h_chain<C>(ctx, j.local, nc, n);
           if (r) return r;
-          if (ctx->device == dev0)
+          if (!cross_device(ctx->device, dev0))
             GM_HIP(hipMemcpyAsync(j.dst, j.local, 32 * n, hipMemcpyDeviceToDevice, ctx->stream));
           else
             GM_HIP(hipMemcpyPeerAsync(j.dst, dev0, j.local, ctx->device, 32 * n, ctx->stream));
@@ -1553,7 +1564,7 @@ int g16_prove_multi_t(gm_multi* m, gm_g16_pk_multi* mp, const uint8_t* wires, co
           if (!pe->nbZ) continue;
           const void* src = (const char*)x->da + 32 * pe->zlo;
           const int dev_e = m->ctx[e]->device;
-          if (dev_e == ctx->device)
+          if (!cross_device(dev_e, ctx->device))
             GM_HIP(hipMemcpyAsync(hz[e], src, 32 * pe->nbZ, hipMemcpyDeviceToDevice, ctx->aux));
           else
             GM_HIP(hipMemcpyPeerAsync(hz[e], dev_e, src, ctx->device, 32 * pe->nbZ, ctx->aux));

@@ -138,8 +138,11 @@ template <class C, bool G2>
 int msm_finish(gm_ctx* ctx, MsmTail& t, typename GroupSel<C, G2>::HF (&jac_out)[3]);
 // plan + launch (points converted into `arena` first unless points_internal)
 template <class C, bool G2>
+// inputs_read (optional) is recorded on ctx->stream once the caller's scalars
+// and points have been read for the last time (after the digits / conversion).
 int msm_device_launch(gm_ctx* ctx, Arena& arena, const void* scalars_dev, const void* points_dev, size_t n,
-                      bool points_internal, const MsmPrecomp* pre, MsmTail& t);
+                      bool points_internal, const MsmPrecomp* pre, MsmTail& t,
+                      hipEvent_t inputs_read = nullptr);
 
 // out = sum_i int(scalars[i]) * points[i] as a host Jacobian triple (X, Y, Z).
 // points_dev is gnark-layout affine points, or (points_internal) an array of

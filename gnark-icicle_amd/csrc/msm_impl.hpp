@@ -1301,7 +1301,7 @@ int msm_run(gm_ctx* ctx, const MsmPlan& plan, const void* points_internal,
 
 template <class C, bool G2>
 int msm_device_launch(gm_ctx* ctx, Arena& arena, const void* scalars_dev, const void* points_dev, size_t n,
-                      bool points_internal, const MsmPrecomp* pre, MsmTail& t) {
+                      bool points_internal, const MsmPrecomp* pre, MsmTail& t, hipEvent_t inputs_read) {
   using DF = typename GroupSel<C, G2>::DF;
   int rc;
   const void* pts = points_dev;
@@ -1327,6 +1327,9 @@ int msm_device_launch(gm_ctx* ctx, Arena& arena, const void* scalars_dev, const 
   }
   MsmPlan plan;
   if ((rc = msm_plan<C>(ctx, arena, scalars_dev, n, pre, plan, glv))) return rc;
+  // the caller's scalars (digits) and gnark-layout points (conversion) are not
+  // read past this point
+  if (inputs_read) GM_HIP(hipEventRecord(inputs_read, ctx->stream));
   return msm_launch<C, G2>(ctx, arena, plan, pts, t);
 }
 
@@ -1382,7 +1385,7 @@ int msm_precompute_points(gm_ctx* ctx, const void* gnark_points, size_t n, const
   template int msm_launch<C, G2>(gm_ctx*, Arena&, const MsmPlan&, const void*, MsmTail&);      \
   template int msm_finish<C, G2>(gm_ctx*, MsmTail&, typename GroupSel<C, G2>::HF (&)[3]);     \
   template int msm_device_launch<C, G2>(gm_ctx*, Arena&, const void*, const void*, size_t, bool, \
-                                        const MsmPrecomp*, MsmTail&);                          \
+                                        const MsmPrecomp*, MsmTail&, hipEvent_t);              \
   template int msm_device<C, G2>(gm_ctx*, const void*, const void*, size_t,                    \
                                  typename GroupSel<C, G2>::HF (&)[3], bool, const MsmPrecomp*);
 #define GM_MSM_INSTANTIATE_PLAN(C) \

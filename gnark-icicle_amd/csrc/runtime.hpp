@@ -83,6 +83,10 @@ struct gm_ctx {
   // the device -- one's sort / reduction (HBM / latency-bound) runs beside
   // another's accumulation (VALU-bound).  Created on first use.
   hipStream_t slot_stream[MSM_SLOTS] = {};
+  // gm_msm_async handles not yet waited for: gm_destroy drains their device work,
+  // releases their slot / readback buffer and orphans them (gm_msm_wait then
+  // fails with GM_ERR_INVALID and frees the handle)
+  std::vector<gm_msm_pending*> live_msms;
   // a / b / c of a host-input prove (gm_g16_prove): their own allocation, outside
   // the workspace arena.  The runtime orders a pageable copy into an allocation
   // after the queued commands that use the same allocation, so copies into an

@@ -3,6 +3,7 @@
 // the proving path.
 #include "curves.hpp"
 #include "runtime.hpp"
+#include "../../include/gnark_mi355x_testhooks.h"
 
 namespace gm {
 

@@ -47,8 +47,7 @@ SYMBOLS = [
     "gm_poly_ops", "gm_reverse_scalars", "gm_groth16_compute_h", "gm_g16_pk_upload", "gm_g16_pk_upload_ex", "gm_g16_pk_upload_shard",
     "gm_g16_partial_bytes", "gm_g16_prove_partial", "gm_g16_finish",
     "gm_g16_pk_free", "gm_g16_pk_precomputed", "gm_g16_prove", "gm_g16_prove_device", "gm_jac_add", "gm_jac_to_affine",
-    "gm_batch_mul_base", "gm_random_scalars", "gm_generator", "gm_test_field_op",
-    "gm_test_point_op", "gm_icicle_generate_twiddles", "gm_icicle_intt_on_device", "gm_icicle_ntt_on_device",
+    "gm_batch_mul_base", "gm_random_scalars", "gm_generator", "gm_icicle_generate_twiddles", "gm_icicle_intt_on_device", "gm_icicle_ntt_on_device",
     "gm_icicle_poly_ops", "gm_device_count", "gm_multi_init", "gm_multi_destroy", "gm_multi_size",
     "gm_multi_context", "gm_g16_pk_upload_multi", "gm_g16_pk_free_multi", "gm_g16_prove_multi",
     "gm_g16_pk_upload_dump", "gm_g16_pk_upload_dump_shard", "gm_g16_pk_save_cache", "gm_g16_pk_load_cache",
@@ -56,6 +55,9 @@ SYMBOLS = [
     "gm_g16_stage_free", "gm_msm_async", "gm_msm_wait", "gm_r1cs_upload", "gm_r1cs_free", "gm_r1cs_eval",
     "gm_g16_prove_r1cs",
 ]
+# test-only library (include/gnark_mi355x_testhooks.h, libgnark_mi355x_testhooks.so)
+TEST_SYMBOLS = ["gm_test_field_op", "gm_test_point_op"]
+TESTHOOKS_PATH = os.path.join(os.path.dirname(LIB_PATH), "libgnark_mi355x_testhooks.so")
 
 
 class GmError(RuntimeError):
@@ -63,6 +65,25 @@ class GmError(RuntimeError):
 
 
 _lib = None
+_testhooks = None
+
+
+def load_testhooks(path: str = None):
+    """The test-only element-wise hooks (parity tests of the field / curve layer);
+    loads the product library first (the hooks link against it)."""
+    global _testhooks
+    if _testhooks is not None:
+        return _testhooks
+    load_library()
+    path = path or TESTHOOKS_PATH
+    if not os.path.exists(path):
+        raise GmError(f"{path} not built -- run `make -C gnark-icicle_amd`")
+    T = ctypes.CDLL(path)
+    vp, sz, i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+    T.gm_test_field_op.argtypes = [vp, i, i, i, vp, vp, vp, sz]
+    T.gm_test_point_op.argtypes = [vp, i, i, i, vp, vp, vp, sz]
+    _testhooks = T
+    return T
 
 
 def load_library(path: str = LIB_PATH):
@@ -123,8 +144,6 @@ def load_library(path: str = LIB_PATH):
     L.gm_batch_mul_base.argtypes = [vp, i, i, vp, vp, sz, vp]
     L.gm_random_scalars.argtypes = [vp, i, u64, sz, vp]
     L.gm_generator.argtypes = [i, i, vp]
-    L.gm_test_field_op.argtypes = [vp, i, i, i, vp, vp, vp, sz]
-    L.gm_test_point_op.argtypes = [vp, i, i, i, vp, vp, vp, sz]
     L.gm_icicle_generate_twiddles.argtypes = [vp, i, sz, i, pvp]
     L.gm_icicle_intt_on_device.argtypes = [vp, i, vp, sz, i, pvp]
     L.gm_icicle_ntt_on_device.argtypes = [vp, i, vp, vp, sz, i]
@@ -435,7 +454,7 @@ class Context:
         O = self.malloc(len(a))
         esz = {0: 32, 1: FP_BYTES[curve_id(curve)], 2: 2 * FP_BYTES[curve_id(curve)]}[kind]
         try:
-            _check(load_library().gm_test_field_op(self.handle, curve_id(curve), kind, op, A.ptr, B.ptr, O.ptr,
+            _check(load_testhooks().gm_test_field_op(self.handle, curve_id(curve), kind, op, A.ptr, B.ptr, O.ptr,
                                                    len(a) // esz))
             return O.to_host()
         finally:
@@ -446,7 +465,7 @@ class Context:
         A, B = self.copy_to_device(a), self.copy_to_device(b)
         O = self.malloc(len(a))
         try:
-            _check(load_library().gm_test_point_op(self.handle, curve_id(curve), int(g2), op, A.ptr, B.ptr,
+            _check(load_testhooks().gm_test_point_op(self.handle, curve_id(curve), int(g2), op, A.ptr, B.ptr,
                                                    O.ptr, len(a) // point_bytes(curve, g2)))
             return O.to_host()
         finally:

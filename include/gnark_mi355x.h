@@ -97,10 +97,16 @@ int gm_msm(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const void* 
  * runs on a stream of its own (GM_MSM_SLOT_STREAMS=0: the context stream), so
  * one MSM's reduction overlaps the next one's accumulation when the process has
  * a hardware queue per stream (GPU_MAX_HW_QUEUES=8 before HIP initialises;
- * HIP's default 4 serialises them).  Synchronous calls
+ * HIP's default 4 serialises them; the library raises the process default to 8
+ * at load time when the variable is unset).  Synchronous calls
  * (gm_msm, gm_msm_prepared, gm_ntt, ...) may be made on the same context while
  * async MSMs are pending: each pending MSM keeps its own scratch arena and its
- * own pinned readback buffer until its gm_msm_wait. */
+ * own pinned readback buffer until its gm_msm_wait, and work queued on the
+ * context after gm_msm_async returns starts only once that MSM has read its
+ * scalars and points, so such a call may overwrite them in place.
+ * gm_destroy with MSMs pending waits for their device work and releases their
+ * resources; each pending handle stays allocated, and its gm_msm_wait returns
+ * GM_ERR_INVALID ("context was destroyed") and frees it. */
 typedef struct gm_msm_pending gm_msm_pending;
 int gm_msm_async(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const void* points_dev, size_t n,
                  gm_msm_pending** out);
@@ -396,13 +402,9 @@ int gm_random_scalars(gm_ctx* ctx, int curve, uint64_t seed, size_t n, void* sca
 /* Generator points of the curve in gnark affine layout (host). */
 int gm_generator(int curve, int g2, void* affine_out);
 
-/* ---- test hooks (element-wise device primitives; parity tests only) ---
- * kind: 0 = Fr, 1 = Fp, 2 = Fp2; op: 0 mul, 1 add, 2 sub, 3 neg, 4 inv, 5 sqr.
- * Point op (affine in/out): 0 mixed add, 1 double, 2 XYZZ add, 3 [1000003]P. */
-int gm_test_field_op(gm_ctx* ctx, int curve, int kind, int op, const void* a_dev,
-                     const void* b_dev, void* out_dev, size_t n);
-int gm_test_point_op(gm_ctx* ctx, int curve, int g2, int op, const void* a_dev,
-                     const void* b_dev, void* out_dev, size_t n);
+/* Element-wise test hooks of the device field / curve layer live in a separate
+ * test-only library (include/gnark_mi355x_testhooks.h,
+ * libgnark_mi355x_testhooks.so); the product library does not export them. */
 
 #ifdef __cplusplus
 }

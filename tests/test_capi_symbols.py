@@ -10,11 +10,13 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "gnark_mi355x.h")
+TEST_HEADER = os.path.join(ROOT, "include", "gnark_mi355x_testhooks.h")
 LIB = os.path.join(ROOT, "gnark-icicle_amd", "libgnark_mi355x.so")
+TLIB = os.path.join(ROOT, "gnark-icicle_amd", "libgnark_mi355x_testhooks.so")
 
 
-def _declared():
-    src = open(HEADER).read()
+def _declared(header=HEADER):
+    src = open(header).read()
     return sorted(set(re.findall(r"\b(gm_[a-z0-9_]+)\s*\(", src)))
 
 
@@ -40,6 +42,35 @@ def test_library_exports_every_declared_symbol(lib):
 def test_python_binding_symbol_list_matches_header():
     import gnark_mi355x as gm
     assert sorted(gm.SYMBOLS) == _declared()
+    assert sorted(gm.TEST_SYMBOLS) == _declared(TEST_HEADER)
+
+
+def test_test_hooks_live_outside_the_product_library(lib):
+    """The element-wise test hooks are a separate test-only library; the product
+    library exports none of them."""
+    tests_only = _declared(TEST_HEADER)
+    assert tests_only and not set(tests_only) & set(_declared())
+    assert not [n for n in tests_only if hasattr(lib, n)]
+    assert os.path.exists(TLIB)
+    t = ctypes.CDLL(TLIB)
+    assert all(hasattr(t, n) for n in tests_only)
+    nm = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True).stdout
+    assert "k_field_op" not in nm and "k_point_op" not in nm
+
+
+def test_library_sets_hw_queue_default_at_load():
+    """The library's load-time constructor gives the process 8 HIP hardware
+    queues when GPU_MAX_HW_QUEUES is unset (so in-flight MSMs overlap without
+    the host setting anything) and leaves a value the process chose alone."""
+    import sys
+    code = ("import ctypes, sys; ctypes.CDLL(sys.argv[1]); libc = ctypes.CDLL(None); "
+            "libc.getenv.restype = ctypes.c_char_p; print(libc.getenv(b'GPU_MAX_HW_QUEUES'))")
+    env = {k: v for k, v in os.environ.items() if k != "GPU_MAX_HW_QUEUES"}
+    out = subprocess.run([sys.executable, "-c", code, LIB], env=env, capture_output=True, text=True, check=True)
+    assert out.stdout.strip() == "b'8'"
+    env["GPU_MAX_HW_QUEUES"] = "4"
+    out = subprocess.run([sys.executable, "-c", code, LIB], env=env, capture_output=True, text=True, check=True)
+    assert out.stdout.strip() == "b'4'"
 
 
 def test_host_helpers_without_gpu(lib):

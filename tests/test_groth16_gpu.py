@@ -177,6 +177,34 @@ def test_groth16_multi_contexts_small(gm_ctx, oracle, cname, k, ndev):
     assert oracle.g16_check(cname, r1, tox, enc(W), rb, sb, *got) == 7
 
 
+@pytest.mark.parametrize("cname,precompute", [("bn254", False), ("bn254", True), ("bls12377", False)])
+def test_groth16_multi_forced_peer_copies(gm_ctx, oracle, monkeypatch, cname, precompute):
+    """The peer-copy branches of the multi-device prover -- b / c of computeH
+    copied to device 0 (groth16.hip compute_h chains) and the h slices copied to
+    the Z-MSM shards (hipMemcpyPeerAsync) -- forced on the one-GPU box with
+    GM_MULTI_FORCE_PEER=1 (4 contexts of device 0): the proof is byte-identical
+    to the oracle's."""
+    import gnark_mi355x as gm
+    monkeypatch.setenv("GM_MULTI_FORCE_PEER", "1")
+    c = pyref.CURVES[cname]
+    r1, W = R.squaring_chain(2000 if cname == "bn254" else 511, cname, x=5)
+    tox = R.encode_vec(cname, [t % c.r for t in TOXIC])
+    pk = oracle.g16_setup(cname, r1, tox)
+    a, b, cc = r1.solve_abc(W)
+    enc = lambda v: R.encode_vec(cname, v)
+    rb, sb = enc([0x3131]), enc([0x4242])
+    exp = oracle.g16_prove(cname, pk, r1.nb_public, enc(W), enc(a), enc(b), enc(cc), rb, sb)
+    with gm.Multi([0] * 4) as m:
+        mpk = gm.ProvingKeyMulti(m, cname, pk, r1.domain_size, r1.nb_wires, r1.nb_public, precompute=precompute)
+        try:
+            got = mpk.prove(enc(W), enc(a), enc(b), enc(cc), rb, sb)
+            got2 = mpk.prove(enc(W), enc(a), enc(b), enc(cc), rb, sb)
+        finally:
+            mpk.free()
+    assert got == exp and got2 == exp
+    assert oracle.g16_check(cname, r1, tox, enc(W), rb, sb, *got) == 7
+
+
 @pytest.mark.parametrize("cname,ncommit,precompute", [("bn254", 1, False), ("bn254", 2, True),
                                                       ("bls12377", 2, False)])
 def test_groth16_bsb22_commitments(gm_ctx, oracle, cname, ncommit, precompute):

@@ -463,6 +463,73 @@ def test_msm_async_interleaved_with_sync(gm_ctx, oracle):
             d[3].free()
 
 
+def test_msm_async_inputs_overwritten_in_place(gm_ctx, oracle):
+    """A synchronous call queued after gm_msm_async may overwrite the pending
+    MSM's scalars and points in place (include/gnark_mi355x.h): the context
+    stream waits until the MSM has read them (after its digits and point
+    conversion), while the accumulation and reduction still run on the MSM's
+    own stream.  Here an in-place gm_ntt over the scalars and a d2d copy over the
+    points follow each of two pending 2^20 MSMs at once; both results are the
+    oracle's MSM of the ORIGINAL inputs, and the overwrites did happen."""
+    import gnark_mi355x as gm
+    n = 1 << 20
+    ins = []
+    for k in range(2):
+        S = gm_ctx.random_scalars("bn254", n, seed=0xE0 + k)
+        K = gm_ctx.random_scalars("bn254", n, seed=0xF0 + k)
+        P = gm_ctx.batch_mul_base("bn254", False, gm.generator("bn254"), K, n)
+        ins.append((S, P, K, S.to_host(), P.to_host()))
+    try:
+        exp = [oracle.msm("bn254", False, sh, ph) for _, _, _, sh, ph in ins]
+        junk = gm_ctx.random_scalars("bn254", 2 * n, seed=0xAB)  # 64 B per point of junk
+        pend = []
+        for S, P, K, sh, ph in ins:
+            pend.append(gm_ctx.msm_async("bn254", S, P, n))
+            gm_ctx.ntt("bn254", S, n, False, False, False)          # scalars overwritten in place
+            gm.load_library().gm_memcpy_d2d(gm_ctx.handle, P.ptr, junk.ptr, 64 * n)  # points overwritten
+        got = [p.wait()[1] for p in pend]
+        assert got == exp
+        assert ins[0][0].to_host() == oracle.fft("bn254", ins[0][3], 0, 0, 0)
+        assert ins[1][1].to_host() == junk.to_host()
+        junk.free()
+    finally:
+        for S, P, K, _, _ in ins:
+            for b in (S, P, K):
+                b.free()
+
+
+def test_gm_destroy_with_msms_pending(oracle):
+    """gm_destroy with two gm_msm_async MSMs pending: it waits for their device
+    work and releases their slot arenas and readback buffers before freeing the
+    context (capi.hip gm_destroy / orphan_pending_msms); each handle's
+    gm_msm_wait then reports the destroyed context and frees the handle.  The
+    inputs may be freed while the MSMs are pending (they have been read once the
+    context stream is past gm_msm_async).  A fresh context afterwards works."""
+    import gnark_mi355x as gm
+    n = 1 << 18
+    ctx = gm.Context(0)
+    S = ctx.random_scalars("bn254", n, seed=0x77)
+    K = ctx.random_scalars("bn254", n, seed=0x78)
+    P = ctx.batch_mul_base("bn254", False, gm.generator("bn254"), K, n)
+    K.free()
+    a = ctx.msm_async("bn254", S, P, n)
+    b = ctx.msm_async("bn254", S, P, n, False)
+    S.free()
+    P.free()
+    ctx.close()
+    for p in (a, b):
+        with pytest.raises(gm.GmError, match="destroyed"):
+            p.wait()
+    with gm.Context(0) as c2:
+        S = c2.random_scalars("bn254", 3000, seed=0x79)
+        K = c2.random_scalars("bn254", 3000, seed=0x7A)
+        P = c2.batch_mul_base("bn254", False, gm.generator("bn254"), K, 3000)
+        pend = c2.msm_async("bn254", S, P, 3000)
+        assert pend.wait()[1] == oracle.msm("bn254", False, S.to_host(), P.to_host())
+        for x in (S, K, P):
+            x.free()
+
+
 def _glv_bls12377():
     import importlib.util
     spec = importlib.util.spec_from_file_location(

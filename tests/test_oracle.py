@@ -281,3 +281,63 @@ def test_bn254_glv_constants_pinned_by_reference():
     assert _hpp_array("beta29_g2", "GlvBn254") == r29(d["beta"] * d["beta"] % p)
     # the lattice basis the device splits with: a + b lambda = 0 mod r
     assert (d["a1"] + d["b1"] * d["lam"]) % r == 0 and (d["a2"] + d["b2"] * d["lam"]) % r == 0
+
+
+def _hpp_u64(name, struct):
+    """The `static constexpr uint64_t` constants `name` of `struct` (msm_impl.hpp)."""
+    import re
+    src = open(os.path.join(HERE, "..", "gnark-icicle_amd", "csrc", "msm_impl.hpp")).read()
+    body = src[src.index("struct %s {" % struct):]
+    body = body[:body.index("\n};")]
+    return int(re.search(r"\b%s = (0x[0-9a-fA-F]+)ull" % name, body).group(1), 16)
+
+
+def _hpp_u64_array(name, struct):
+    import re
+    src = open(os.path.join(HERE, "..", "gnark-icicle_amd", "csrc", "msm_impl.hpp")).read()
+    body = src[src.index("struct %s {" % struct):]
+    body = body[:body.index("\n};")]
+    fn = body[body.index(name + "(int i)"):]
+    lit = fn[fn.index("{", fn.index("a[")) + 1:fn.index("};")]
+    return [int(x[:-3], 16) for x in re.findall(r"0x[0-9a-fA-F]+ull", lit)]
+
+
+def test_bls12377_glv_constants_pinned_by_reference():
+    """The BLS12-377 GLV endomorphism of the MSM (csrc/msm_impl.hpp GlvBls377)
+    is exactly the one the reference holds in std/algebra/native/sw_bls12377/
+    inner.go:58-63: lambda = bls12377lambda, and phi1 (inner.go:26-30, G1)
+    multiplies x by thirdRootOne1 while phi2 (:38-42, the G2 twist) multiplies
+    by thirdRootOne2 = thirdRootOne1^2 (inner.go:63).  The device's lambda
+    (LAM_HI:LAM_LO), its split constant g = floor(2^384 / lambda), and its
+    radix-2^29 Montgomery beta / beta^2 (R = 2^406) encode exactly these, and
+    [lambda] P = (thirdRootOne1 x, y) holds on G1 and G2 points."""
+    c = pyref.CURVES["bls12377"]
+    p, r = c.p, c.r
+    lam_ref = int.from_bytes(bytes([0x45, 0x22, 0x17, 0xcc, 0x90, 0x00, 0x00, 0x01, 0x0a, 0x11, 0x80, 0x00,
+                                    0x00, 0x00, 0x00, 0x00]), "big")
+    t1_ref = int.from_bytes(bytes([
+        0x09, 0xb3, 0xaf, 0x05, 0xdd, 0x14, 0xf6, 0xec, 0x61, 0x9a, 0xaf, 0x7d, 0x34, 0x59,
+        0x4a, 0xab, 0xc5, 0xed, 0x13, 0x47, 0x97, 0x0d, 0xec, 0x00, 0x45, 0x22, 0x17, 0xcc,
+        0x90, 0x00, 0x00, 0x00, 0x85, 0x08, 0xc0, 0x00, 0x00, 0x00, 0x00, 0x01]), "big")
+    t2_ref = t1_ref * t1_ref % p
+    lam_dev = (_hpp_u64("LAM_HI", "GlvBls377") << 64) | _hpp_u64("LAM_LO", "GlvBls377")
+    assert lam_dev == lam_ref
+    g = _hpp_u64_array("g", "GlvBls377")
+    assert sum(v << (64 * i) for i, v in enumerate(g)) == (1 << 384) // lam_ref
+
+    def r29(x):
+        v = x * (1 << (29 * 14)) % p
+        return [(v >> (29 * i)) & ((1 << 29) - 1) for i in range(14)]
+    assert _hpp_array("beta29", "GlvBls377") == r29(t1_ref)
+    assert _hpp_array("beta29_g2", "GlvBls377") == r29(t2_ref)
+    # the reference's pair is an endomorphism of both groups
+    G1, G2 = pyref.Group(c, False), pyref.Group(c, True)
+    P = G1.mul(G1.generator(), 0x7654321)
+    assert G1.mul(P, lam_ref) == (t1_ref * P[0] % p, P[1])
+    Q = G2.mul(G2.generator(), 0x1234)
+    LQ = G2.mul(Q, lam_ref)
+    assert LQ == ((Q[0][0] * t2_ref % p, Q[0][1] * t2_ref % p), Q[1])
+    # and the derivation tool agrees
+    d = _glv_module().derive_bls12377()
+    assert (d["lam"], d["beta"], d["beta_g2"]) == (lam_ref, t1_ref, t2_ref)
+    assert (lam_ref * lam_ref + lam_ref + 1) % r == 0
