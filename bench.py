@@ -371,7 +371,12 @@ def secondary(ctx, gm, args):
         res["groth16"] = []
         for l in (int(x) for x in args.g16_logn.split(",") if x):
             if l in plain:
-                res["groth16"].append(groth16_bench(ctx, gm, l, precompute=False, check_oracle=(l <= 20)))
+                # <= 2^20: every scope checked against the oracle, plus the key I/O; the
+                # plain 2^24 key: the staged scopes and ONE oracle prove of the host-input
+                # proof (its check and the labelled CPU baseline of the headline workload)
+                res["groth16"].append(groth16_bench(ctx, gm, l, precompute=False,
+                                                    check_oracle=("full" if l <= 20 else
+                                                                  "host" if not args.no_cpu_baseline else None)))
             if not args.g16_no_precomputed:
                 res["groth16"].append(groth16_bench(ctx, gm, l, precompute=True))
     return res
@@ -455,8 +460,11 @@ def groth16_bench(ctx, gm, logn, precompute=True, check_oracle=False):
       host:   wires / a / b / c in host memory, gm_g16_prove -- the scope of
               icicle.go:204-412 (its H2D copies of a, b, c and wA / wB included);
       device: the same vectors already resident (gm_g16_prove_device).
-    check_oracle: the timed host-scope proof is compared with the oracle prover
-    (prove.go:62-325 restatement) on the same key and inputs."""
+    check_oracle: "full" -- the timed host-scope and R1CS-resident proofs are
+    compared with the oracle prover (prove.go:62-325 restatement) on the same key
+    and inputs, plus the staged scopes and the key I/O; "host" -- the staged
+    scopes and the host-scope proof only (one oracle prove: the 2^24 headline's
+    check and CPU baseline)."""
     import numpy as np
     n = 1 << logn
     nb_wires = n + 2
@@ -498,20 +506,44 @@ def groth16_bench(ctx, gm, logn, precompute=True, check_oracle=False):
         t0 = time.perf_counter()
         proof_r1cs = dpk.prove_r1cs(ch, host[0], r[:32], r[32:])
         t_r1cs.append(time.perf_counter() - t0)
+    # R1CS resident + wires staged during Solve (the wire-extended level hook: 64
+    # pieces put before the timer), then gm_g16_stage_prove_r1cs: nothing crosses
+    # PCIe after Solve
+    t_r1cs_staged, proof_r1cs_staged = [], None
+    nw = nb_wires
+    for i in range(reps + 1):
+        st = dpk.stage(n)
+        wstep = max(1, nw // 64)
+        for lo in range(0, nw, wstep):
+            st.put_range(st.WIRES, lo, host[0][32 * lo:32 * min(nw, lo + wstep)])
+        ctx.synchronize()
+        time.sleep(0.05)  # the staged copies finish during "Solve"
+        t0 = time.perf_counter()
+        proof_r1cs_staged = st.prove_r1cs(ch, r[:32], r[32:])
+        if i:
+            t_r1cs_staged.append(time.perf_counter() - t0)
+        st.free()
     ch.free()
     med = lambda v: sorted(v)[len(v) // 2]
     res = {"logn": logn, "pk": "precomputed" if precompute else "plain",
            "roofline": groth16_roofline(n, nb_wires, precompute, med(t_dev)),
            "prove_ms_host_inputs": round(med(t_host) * 1e3, 3), "prove_ms_device_inputs": round(med(t_dev) * 1e3, 3),
            "prove_ms_r1cs_resident": round(med(t_r1cs) * 1e3, 3),
+           "prove_ms_r1cs_resident_wires_staged": round(med(t_r1cs_staged) * 1e3, 3),
+           "r1cs_staged_matches_r1cs_resident": bool(proof_r1cs_staged == proof_r1cs),
            "best_ms": {"host_inputs": round(min(t_host) * 1e3, 3), "device_inputs": round(min(t_dev) * 1e3, 3),
-                       "r1cs_resident": round(min(t_r1cs) * 1e3, 3)},
+                       "r1cs_resident": round(min(t_r1cs) * 1e3, 3),
+                       "r1cs_resident_wires_staged": round(min(t_r1cs_staged) * 1e3, 3)},
            "runs": reps, "warmup": 1, "stat": "median",
            "scope": "host_inputs = icicle.go:204-412 incl. H2D of wires/a/b/c; device_inputs = same with inputs "
                     "resident; r1cs_resident = host wires only (a/b/c from the device-resident R1CS, "
-                    "gm_g16_prove_r1cs); all after Solve"}
+                    "gm_g16_prove_r1cs); r1cs_resident_wires_staged = the same with the wires staged during "
+                    "Solve (gm_g16_stage_prove_r1cs, the Go default path with the wire level hook); all after "
+                    "Solve"}
     if check_oracle:
-        res.update(staged_and_io_bench(ctx, gm, dpk, pk, n, nb_wires, nb_public, host, r, proof))
+        res.update(staged_bench(ctx, dpk, n, host, r, proof))
+    if check_oracle == "full":
+        res.update(io_bench(ctx, gm, dpk, pk, n, nb_wires, nb_public, host, r, proof))
     dpk.free()
     for b in [W, A, B, C] + srcs:
         b.free()
@@ -525,14 +557,15 @@ def groth16_bench(ctx, gm, logn, precompute=True, check_oracle=False):
                                    nthreads=threads)
         cpu_s = time.perf_counter() - t0
         res["matches_oracle"] = bool(exp == proof)
-        # the R1CS-resident proof: a, b, c of the chain from the same wires
-        wv = host[0].reshape(nb_wires, 32)
-        ca = np.concatenate([wv[2:n + 1], wv[0:1]])
-        cb = np.concatenate([wv[2:n + 1], wv[n + 1:n + 2]])
-        cc = np.concatenate([wv[3:n + 2], wv[1:2]])
-        exp_r1cs = oracle_lib.g16_prove("bn254", pk, nb_public, host[0], ca.tobytes(), cb.tobytes(), cc.tobytes(),
-                                        r[:32], r[32:], nthreads=threads)
-        res["r1cs_resident_matches_oracle"] = bool(exp_r1cs == proof_r1cs)
+        if check_oracle == "full":
+            # the R1CS-resident proof: a, b, c of the chain from the same wires
+            wv = host[0].reshape(nb_wires, 32)
+            ca = np.concatenate([wv[2:n + 1], wv[0:1]])
+            cb = np.concatenate([wv[2:n + 1], wv[n + 1:n + 2]])
+            cc = np.concatenate([wv[3:n + 2], wv[1:2]])
+            exp_r1cs = oracle_lib.g16_prove("bn254", pk, nb_public, host[0], ca.tobytes(), cb.tobytes(),
+                                            cc.tobytes(), r[:32], r[32:], nthreads=threads)
+            res["r1cs_resident_matches_oracle"] = bool(exp_r1cs == proof_r1cs)
         # the labelled CPU baseline of this workload (BASELINE.md §2.1 asks for
         # groth16_bn254.Prove beside the GPU; no Go on the box -> the port)
         res["cpu_baseline"] = {
@@ -600,34 +633,58 @@ def groth16_roofline(n, nb_wires, precompute, t_s):
                                                              MADS_G1_ADD, MADS_G2_ADD)}}
 
 
-def staged_and_io_bench(ctx, gm, dpk, pk, n, nb_wires, nb_public, host, r, host_proof):
-    """SURVEY.md §8f rows 3-4 on the same key:
-      staged: a / b / c handed over in 64 "solver levels" and the wires in one
-              range before the timer starts (they overlap Solve), then the timed
-              gm_g16_stage_prove -- the prover latency left after Solve;
+def staged_bench(ctx, dpk, n, host, r, host_proof):
+    """SURVEY.md §8f row 4 on the same key (gm_g16_stage_*), a / b / c handed over
+    in 64 "solver levels" before the timer starts (the level hook runs them
+    during Solve), then two timed scopes after Solve:
+      wires_after_solve: the wires copied inside the timer, then the prove -- the
+              Go staged path as integration/go/icicle_bn254/staged.go runs it
+              (its prove(): PutRange(StageWires) then Prove);
+      all_during_solve:  the wires also staged during Solve (64 ranges, as the
+              wire-extended level hook hands them over), only the prove timed.
+    The first stage of each scope is an untimed warm-up (the key keeps the stage
+    buffers for the next proof)."""
+    out = {}
+    reps = 3
+    proofs = {}
+    for scope in ("wires_after_solve", "all_during_solve"):
+        ts = []
+        for i in range(reps + 1):
+            st = dpk.stage(n)
+            step = max(1, n // 64)
+            for lo in range(0, n, step):
+                for which, v in ((st.A, host[1]), (st.B, host[2]), (st.C, host[3])):
+                    st.put_range(which, lo, v[32 * lo:32 * (lo + step)])
+            nw = len(host[0]) // 32
+            if scope == "all_during_solve":
+                wstep = max(1, nw // 64)
+                for lo in range(0, nw, wstep):
+                    st.put_range(st.WIRES, lo, host[0][32 * lo:32 * min(nw, lo + wstep)])
+            ctx.synchronize()
+            time.sleep(0.05)  # the staged copies finish during "Solve"
+            t0 = time.perf_counter()
+            if scope == "wires_after_solve":
+                st.put_range(st.WIRES, 0, host[0])
+            proof = st.prove(r[:32], r[32:])
+            if i:
+                ts.append(time.perf_counter() - t0)
+            st.free()
+        out["prove_ms_staged_" + scope] = round(sorted(ts)[reps // 2] * 1e3, 3)
+        proofs[scope] = proof
+    out["staged_matches_host_scope"] = bool(all(p == host_proof for p in proofs.values()))
+    out["staged_scope"] = ("a/b/c staged by level before the timer in both; wires_after_solve = staged.go's "
+                           "prove() (wires H2D + prove), all_during_solve = prove only")
+    return out
+
+
+def io_bench(ctx, gm, dpk, pk, n, nb_wires, nb_public, host, r, proof):
+    """SURVEY.md §8f row 3 on the same key:
       dump:   the key's five point arrays written as WriteDump slices
               (marshal.go:389-456) to a local file, then streamed into device
               buffers (gm_g16_pk_upload_dump) -- file read + H2D + conversion;
       cache:  save / load of the device-layout key (gm_g16_pk_save_cache / load)."""
     import tempfile
-    import numpy as np
     out = {}
-    reps = 3
-    ts = []
-    for _ in range(reps):
-        st = dpk.stage(n)
-        for lo in range(0, n, n // 64):
-            for which, v in ((st.A, host[1]), (st.B, host[2]), (st.C, host[3])):
-                st.put_range(which, lo, v[32 * lo:32 * (lo + n // 64)])
-        st.put_range(st.WIRES, 0, host[0])
-        ctx.synchronize()
-        time.sleep(0.05)  # the copies finish during "Solve"
-        t0 = time.perf_counter()
-        proof = st.prove(r[:32], r[32:])
-        ts.append(time.perf_counter() - t0)
-        st.free()
-    out["prove_ms_staged_after_solve"] = round(sorted(ts)[reps // 2] * 1e3, 3)
-    out["staged_matches_host_scope"] = bool(proof == host_proof)
     meta = {k: pk[k] for k in ("g1_alpha", "g1_beta", "g1_delta", "g2_beta", "g2_delta", "infA", "infB")}
     meta["counts"] = (nb_wires, nb_wires, nb_wires - nb_public)
     with tempfile.TemporaryDirectory() as d:

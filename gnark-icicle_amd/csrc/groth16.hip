@@ -90,6 +90,7 @@ size_t internal_point_bytes(int curve, bool g2) {
 }
 
 void pk_release(gm_g16_pk* pk) {
+  stage_spare_release(pk);
   for (void* q : {pk->A, pk->B, pk->Z, pk->K, pk->B2, pk->idxA, pk->idxB, pk->idxK})
     if (q) hipFree(q);
   delete pk;
@@ -1219,11 +1220,37 @@ int gm_g16_prove(gm_ctx* ctx, gm_g16_pk* pk, const void* wires, const void* a, c
 // Wires alone in host memory, the R1CS resident (gm_r1cs_upload): the wires
 // are copied, a / b / c evaluated on the device (auxiliary stream, ahead of
 // computeH) while the A/B/K MSMs run on the main stream.
+}  // extern "C"
+
+// Proof from device-resident wires and a device-resident R1CS: a, b, c are
+// evaluated into the caller's n-element buffers (gm_g16_prove_r1cs, staged
+// wires: gm_g16_stage_prove_r1cs).  The key / system match is checked by the callers.
+int gm::g16_prove_r1cs_device(gm_ctx* ctx, gm_g16_pk* pk, const gm_r1cs* r1, const void* wires_dev, void* a,
+                              void* b, void* c, const void* r, const void* s, void* ar_out, void* bs_out,
+                              void* krs_out) {
+  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  GM_HIP(hipSetDevice(ctx->device));
+  const size_t nc = r1cs_nb_constraints(r1);
+  int rc = pk->curve == GM_BN254
+               ? g16_prove_t<CurveBN254>(ctx, pk, wires_dev, a, b, c, nullptr, nullptr, nullptr, nc, r, s, ar_out,
+                                         bs_out, krs_out, r1)
+               : g16_prove_t<CurveBLS12377>(ctx, pk, wires_dev, a, b, c, nullptr, nullptr, nullptr, nc, r, s,
+                                            ar_out, bs_out, krs_out, r1);
+  prof_collect(ctx);
+  return rc;
+}
+
+bool gm::r1cs_matches_key(const gm_g16_pk* pk, const gm_r1cs* r1) {
+  return r1cs_nb_constraints(r1) <= pk->n && r1cs_nb_wires(r1) == pk->nb_wires && pk->wlo == 0 &&
+         pk->whi == pk->nb_wires;
+}
+
+extern "C" {
+
 int gm_g16_prove_r1cs(gm_ctx* ctx, gm_g16_pk* pk, const gm_r1cs* r1, const void* wires, const void* r,
                       const void* s, void* ar_out, void* bs_out, void* krs_out) {
   if (!ctx || !pk || !r1 || !wires || !r || !s || !ar_out || !bs_out || !krs_out) return GM_ERR_INVALID;
-  const size_t nc = r1cs_nb_constraints(r1);
-  if (nc > pk->n || r1cs_nb_wires(r1) != pk->nb_wires || pk->wlo != 0 || pk->whi != pk->nb_wires) {
+  if (!r1cs_matches_key(pk, r1)) {
     set_error("prove_r1cs: constraint system does not match the proving key (constraints <= n, same wires, "
               "whole key)");
     return GM_ERR_INVALID;
@@ -1237,12 +1264,7 @@ int gm_g16_prove_r1cs(gm_ctx* ctx, gm_g16_pk* pk, const gm_r1cs* r1, const void*
       (rc = db.alloc(arena, 32 * pk->n)) || (rc = dc.alloc(arena, 32 * pk->n)))
     return rc;
   GM_HIP(hipMemcpyAsync(w.p, wires, 32 * pk->nb_wires, hipMemcpyHostToDevice, ctx->stream));
-  rc = pk->curve == GM_BN254 ? g16_prove_t<CurveBN254>(ctx, pk, w.p, da.p, db.p, dc.p, nullptr, nullptr, nullptr, nc,
-                                                       r, s, ar_out, bs_out, krs_out, r1)
-                             : g16_prove_t<CurveBLS12377>(ctx, pk, w.p, da.p, db.p, dc.p, nullptr, nullptr, nullptr,
-                                                          nc, r, s, ar_out, bs_out, krs_out, r1);
-  prof_collect(ctx);
-  return rc;
+  return gm::g16_prove_r1cs_device(ctx, pk, r1, w.p, da.p, db.p, dc.p, r, s, ar_out, bs_out, krs_out);
 }
 
 // ---- sharded Groth16 (one process per GPU) --------------------

@@ -26,6 +26,10 @@ struct gm_g16_pk {
   // (g16_sums_t).  The compaction maps idxX stay as they are.
   bool wshare[3] = {false, false, false};  // A, B (and B2), K
   gm::MsmPrecomp preW;  // the wire plan's geometry (precomp: c / W / narrow of the shared arrays, stride = span)
+  // staging buffers of the last freed gm_g16_stage of this key (pk_io.hip): the
+  // next gm_g16_stage_begin on the same context reuses them instead of
+  // allocating 4 vectors and the pinned ring per proof
+  gm_g16_stage* spare_stage = nullptr;
 };
 
 namespace gm {
@@ -45,6 +49,7 @@ using PointSource = std::function<int(int which, size_t count, bool g2, const Ms
 int check_curve_id(int curve);
 size_t internal_point_bytes(int curve, bool g2);
 void pk_release(gm_g16_pk* pk);
+void stage_spare_release(gm_g16_pk* pk);  // pk_io.hip
 // gnark-layout points on the device -> internal layout at dst (+ window copies)
 int prepare_points_into(gm_ctx* ctx, int curve, bool g2, const void* gnark_dev, size_t count,
                         const MsmPrecomp* pre, void* dst);
@@ -73,6 +78,11 @@ inline size_t pk_array_points(const gm_g16_pk* pk, int which) {
 // queued on ctx->stream
 int r1cs_eval_device(gm_ctx* ctx, const gm_r1cs* r, const void* wires_dev, void* a, void* b, void* c);
 size_t r1cs_nb_constraints(const gm_r1cs* r);
+// proof from device-resident wires through a device-resident R1CS (groth16.hip);
+// a, b, c: n-element device buffers the evaluation writes
+int g16_prove_r1cs_device(gm_ctx* ctx, gm_g16_pk* pk, const gm_r1cs* r1, const void* wires_dev, void* a, void* b,
+                          void* c, const void* r, const void* s, void* ar_out, void* bs_out, void* krs_out);
+bool r1cs_matches_key(const gm_g16_pk* pk, const gm_r1cs* r1);
 size_t r1cs_nb_wires(const gm_r1cs* r);
 // src == nullptr: points from the host pointers in h
 int pk_upload_ranges(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsigned flags, const Ranges& rg,

@@ -248,6 +248,12 @@ struct gm_g16_stage {
 };
 
 namespace {
+// env knob that is on unless set to 0 (read per call: tests flip it)
+bool getenv_flag_off(const char* name) {
+  const char* v = getenv(name);
+  return v && atoi(v) == 0;
+}
+
 // dst[idx[j]] = val[j] (32-byte Fr)
 // (gm_g16_stage_put_indexed checks every index on the host before the copy;
 // the i < len test only keeps a bad launch from writing out of bounds)
@@ -477,6 +483,17 @@ int gm_g16_pk_load_cache(gm_ctx* ctx, int fd, gm_g16_pk** out) {
 }
 
 // ---- staged inputs ----------------------------------------------------------
+}  // extern "C"
+
+void gm::stage_spare_release(gm_g16_pk* pk) {
+  if (pk->spare_stage) {
+    delete pk->spare_stage;
+    pk->spare_stage = nullptr;
+  }
+}
+
+extern "C" {
+
 int gm_g16_stage_begin(gm_ctx* ctx, gm_g16_pk* pk, size_t nb_constraints, gm_g16_stage** out) {
   if (!ctx || !pk || !out) return GM_ERR_INVALID;
   if (nb_constraints > pk->n) {
@@ -485,6 +502,16 @@ int gm_g16_stage_begin(gm_ctx* ctx, gm_g16_pk* pk, size_t nb_constraints, gm_g16
   }
   std::lock_guard<std::recursive_mutex> g(ctx->mu);
   GM_HIP(hipSetDevice(ctx->device));
+  if (gm_g16_stage* sp = pk->spare_stage; sp && sp->ctx == ctx) {
+    // the key's buffers of a previous proof (gm_g16_stage_free parked them)
+    pk->spare_stage = nullptr;
+    sp->nc = nb_constraints;
+    for (int v = 0; v < 3; v++) sp->len[v] = nb_constraints;
+    sp->next = 0;
+    for (bool& u : sp->used) u = false;
+    *out = sp;
+    return GM_OK;
+  }
   auto* st = new gm_g16_stage();
   st->ctx = ctx;
   st->pk = pk;
@@ -580,11 +607,37 @@ int gm_g16_stage_prove(gm_g16_stage* st, const void* r, const void* s, void* ar_
                              bs_out, krs_out);
 }
 
+int gm_g16_stage_prove_r1cs(gm_g16_stage* st, const gm_r1cs* r1, const void* r, const void* s, void* ar_out,
+                            void* bs_out, void* krs_out) {
+  if (!st || !r1 || !r || !s || !ar_out || !bs_out || !krs_out) return GM_ERR_INVALID;
+  gm_ctx* ctx = st->ctx;
+  if (!r1cs_matches_key(st->pk, r1)) {
+    set_error("stage_prove_r1cs: constraint system does not match the proving key (constraints <= n, same wires, "
+              "whole key)");
+    return GM_ERR_INVALID;
+  }
+  {
+    std::lock_guard<std::recursive_mutex> g(ctx->mu);
+    GM_HIP(hipSetDevice(ctx->device));
+    GM_HIP(hipStreamSynchronize(ctx->copy));
+  }
+  // the stage's a / b / c vectors (n each) receive the R1CS evaluation
+  return g16_prove_r1cs_device(ctx, st->pk, r1, st->vec[3], st->vec[0], st->vec[1], st->vec[2], r, s, ar_out,
+                               bs_out, krs_out);
+}
+
 int gm_g16_stage_free(gm_g16_stage* st) {
   if (!st) return GM_OK;
   std::lock_guard<std::recursive_mutex> g(st->ctx->mu);
   hipSetDevice(st->ctx->device);
   hipStreamSynchronize(st->ctx->copy);
+  // Park the buffers with the key for its next proof (one spare per key): a
+  // fresh stage is 4 hipMallocs of up to n Fr plus 4 x 16 MiB of pinned host
+  // memory.  The prove that used them has returned, so nothing reads them.
+  if (!st->pk->spare_stage && !getenv_flag_off("GM_G16_STAGE_REUSE")) {
+    st->pk->spare_stage = st;
+    return GM_OK;
+  }
   delete st;
   return GM_OK;
 }

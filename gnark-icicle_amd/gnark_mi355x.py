@@ -53,7 +53,7 @@ SYMBOLS = [
     "gm_g16_pk_upload_dump", "gm_g16_pk_upload_dump_shard", "gm_g16_pk_save_cache", "gm_g16_pk_load_cache",
     "gm_g16_stage_begin", "gm_g16_stage_put_range", "gm_g16_stage_put_indexed", "gm_g16_stage_prove",
     "gm_g16_stage_free", "gm_msm_async", "gm_msm_wait", "gm_r1cs_upload", "gm_r1cs_free", "gm_r1cs_eval",
-    "gm_g16_prove_r1cs",
+    "gm_g16_prove_r1cs", "gm_g16_stage_prove_r1cs",
 ]
 # test-only library (include/gnark_mi355x_testhooks.h, libgnark_mi355x_testhooks.so)
 TEST_SYMBOLS = ["gm_test_field_op", "gm_test_point_op"]
@@ -165,6 +165,7 @@ def load_library(path: str = LIB_PATH):
     L.gm_g16_stage_put_indexed.argtypes = [vp, i, vp, vp, sz]
     L.gm_g16_stage_prove.argtypes = [vp, vp, vp, vp, vp, vp]
     L.gm_g16_stage_free.argtypes = [vp]
+    L.gm_g16_stage_prove_r1cs.argtypes = [vp, vp, vp, vp, vp, vp, vp]
     L.gm_msm_async.argtypes = [vp, i, i, vp, vp, sz, pvp]
     L.gm_msm_wait.argtypes = [vp, vp, vp]
     _lib = L
@@ -788,6 +789,17 @@ class Stage:
         krs = np.zeros(point_bytes(self.pk.curve, False), np.uint8)
         bs = np.zeros(point_bytes(self.pk.curve, True), np.uint8)
         _check(load_library().gm_g16_stage_prove(self.handle, _p(R), _p(S), _p(ar), _p(bs), _p(krs)))
+        return ar.tobytes(), bs.tobytes(), krs.tobytes()
+
+    def prove_r1cs(self, r1cs: "R1CS", r: bytes, s: bytes):
+        """gm_g16_stage_prove_r1cs: the wires were staged (during Solve), a, b, c
+        come from the device-resident constraint system."""
+        R, S = _buf(r), _buf(s)
+        ar = np.zeros(point_bytes(self.pk.curve, False), np.uint8)
+        krs = np.zeros(point_bytes(self.pk.curve, False), np.uint8)
+        bs = np.zeros(point_bytes(self.pk.curve, True), np.uint8)
+        _check(load_library().gm_g16_stage_prove_r1cs(self.handle, r1cs.handle, _p(R), _p(S), _p(ar), _p(bs),
+                                                      _p(krs)))
         return ar.tobytes(), bs.tobytes(), krs.tobytes()
 
     def free(self):

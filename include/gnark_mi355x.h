@@ -371,7 +371,10 @@ int gm_g16_pk_load_cache(gm_ctx* ctx, int fd, gm_g16_pk** out);
  * gm_g16_stage_prove waits for the queued copies and proves from the
  * device-resident inputs (gm_g16_prove_device).  Every element of a, b, c
  * [0, nb_constraints) and of the wires [0, nb_wires) must have been put; the
- * prove consumes a, b, c (one proof per stage). */
+ * prove consumes a, b, c (one proof per stage).  gm_g16_stage_free keeps the
+ * stage's device vectors and pinned ring with the key (one spare per key,
+ * released by gm_g16_pk_free), and the next gm_g16_stage_begin on the same
+ * context reuses them: no allocation per proof (GM_G16_STAGE_REUSE=0: off). */
 typedef struct gm_g16_stage gm_g16_stage;
 #define GM_STAGE_A 0
 #define GM_STAGE_B 1
@@ -384,6 +387,12 @@ int gm_g16_stage_put_range(gm_g16_stage* st, int which, size_t lo, size_t count,
 int gm_g16_stage_put_indexed(gm_g16_stage* st, int which, const void* host_base, const uint32_t* idx, size_t k);
 int gm_g16_stage_prove(gm_g16_stage* st, const void* r, const void* s, void* ar_out, void* bs_out,
                        void* krs_out);
+/* The wires-only staged proof of a resident constraint system: the wires were
+ * put during Solve (GM_STAGE_WIRES, e.g. per solver level), a, b, c come from
+ * the device R1CS (gm_r1cs_upload) -- nothing crosses PCIe after Solve.  The
+ * stage's a / b / c need not be put (they receive the evaluation). */
+int gm_g16_stage_prove_r1cs(gm_g16_stage* st, const gm_r1cs* r1cs, const void* r, const void* s, void* ar_out,
+                            void* bs_out, void* krs_out);
 int gm_g16_stage_free(gm_g16_stage* st);
 
 /* ---- host-side group helpers (finishing adds of sharded MSMs) ---------- */

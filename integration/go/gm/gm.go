@@ -408,6 +408,16 @@ func (st *G16Stage) Prove(r, s, ar, bs, krs unsafe.Pointer) error {
 	return nil
 }
 
+// ProveR1CS proves from the staged wires through the resident R1CS r1 (a, b, c
+// are evaluated on the device; gm_g16_stage_prove_r1cs).
+func (st *G16Stage) ProveR1CS(r1 *R1CS, r, s, ar, bs, krs unsafe.Pointer) error {
+	if rc := C.gm_g16_stage_prove_r1cs(st.h, r1.h, r, s, ar, bs, krs); rc != C.GM_OK {
+		return lastErr("gm_g16_stage_prove_r1cs", rc)
+	}
+	return nil
+}
+
+// Free releases the stage (its buffers stay with the key for the next proof).
 func (st *G16Stage) Free() { C.gm_g16_stage_free(st.h) }
 
 // ---------------------------------------------------------------------------

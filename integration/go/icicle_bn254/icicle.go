@@ -230,11 +230,13 @@ func Prove(r1cs *cs.R1CS, pk *ProvingKey, fullWitness witness.Witness, opts ...b
 		solver.OverrideHint(solver.GetHintID(fcs.Bsb22CommitmentComputePlaceholder),
 			bsb22Hint(pk, info, proof, committed, &opt)))
 
-	// -tags mi355x_levelhook: a, b, c move to the GPU level by level during
-	// Solve (staged.go); otherwise beginStaged returns nil (staged_off.go)
+	// -tags mi355x_levelhook: the wires (and a, b, c unless the R1CS is resident)
+	// move to the GPU level by level during Solve (staged.go); otherwise
+	// beginStaged returns nil (staged_off.go)
 	var staged *stagedRun
-	if pk.deviceInfo.r1 == nil && gm.NbDevices() == 1 {
-		st, hookOpt, err := pk.beginStaged(r1cs.GetNbConstraints())
+	if gm.NbDevices() == 1 {
+		nbInputs := r1cs.GetNbPublicVariables() + r1cs.GetNbSecretVariables()
+		st, hookOpt, err := pk.beginStaged(r1cs.GetNbConstraints(), nbInputs, pk.deviceInfo.r1)
 		if err != nil {
 			return nil, err
 		}
@@ -266,7 +268,7 @@ func Prove(r1cs *cs.R1CS, pk *ProvingKey, fullWitness witness.Witness, opts ...b
 		return nil, err
 	}
 
-	if staged != nil { // a, b, c already on the device
+	if staged != nil { // the wires (and a, b, c) already on the device
 		if err := staged.prove(w, &r, &s, unsafe.Pointer(&proof.Ar), unsafe.Pointer(&proof.Bs),
 			unsafe.Pointer(&proof.Krs)); err != nil {
 			return nil, err

@@ -1,14 +1,19 @@
 //go:build icicle && mi355x_levelhook
 
-// Staged variant of Prove (SURVEY.md §8f row 4): a, b, c reach the GPU level
-// by level while the R1CS solver still runs (constraint/bn254/solver.go:
-// 426-532), so the prove after Solve starts from device-resident inputs
-// (gm_g16_stage_*).  Needs the solver patch integration/go/solver_levelhook.diff
-// (csolver.WithLevelHook); build with -tags icicle,mi355x_levelhook.  Prove
-// takes this path when the constraint system is not resident on the device.
+// Staged variant of Prove (SURVEY.md §8f row 4): the solver's results reach the
+// GPU level by level while the R1CS solver still runs (constraint/bn254/solver.go:
+// 426-532), so nothing crosses PCIe after Solve:
+//   - the wires: every level's solved wire ids (wIDs) and the witness inputs,
+//     scattered from solver.values into the stage's wire vector;
+//   - a, b, c: every level's finished constraints, unless the constraint system
+//     is resident on the device (then a, b, c are evaluated there from the staged
+//     wires: gm_g16_stage_prove_r1cs).
+// Needs the solver patch integration/go/solver_levelhook.diff
+// (csolver.WithLevelHook); build with -tags icicle,mi355x_levelhook.
 //
 // NOT COMPILED HERE: this image has no Go toolchain.  The C side is tested by
-// tests/test_pk_io_gpu.py::test_staged_inputs_by_level.
+// tests/test_pk_io_gpu.py::test_staged_inputs_by_level and
+// tests/test_r1cs_gpu.py::test_groth16_stage_prove_r1cs_wires_by_level.
 package icicle_bn254
 
 import (
@@ -22,21 +27,38 @@ import (
 
 // stagedRun is one proof's staging area plus the first error a level hook hit.
 type stagedRun struct {
-	st   *gm.G16Stage
-	perr error
+	st        *gm.G16Stage
+	r1        *gm.R1CS // resident constraint system (a, b, c evaluated on the device), or nil
+	nbInputs  int      // witness wires [0, nbInputs): ONE, public, secret
+	inputsPut bool
+	perr      error
 }
 
 // beginStaged opens a staging area for nbConstraints constraints and returns
-// the solver option that forwards every finished level's a[cID], b[cID],
-// c[cID] to it.
-func (pk *ProvingKey) beginStaged(nbConstraints int) (*stagedRun, csolver.Option, error) {
+// the solver option that forwards every finished level to it.  r1 != nil: the
+// constraint system is resident, only the wires are staged.
+func (pk *ProvingKey) beginStaged(nbConstraints, nbInputs int, r1 *gm.R1CS) (*stagedRun, csolver.Option, error) {
 	st, err := pk.deviceInfo.key.Stage(nbConstraints)
 	if err != nil {
 		return nil, nil, err
 	}
-	run := &stagedRun{st: st}
-	hook := func(cIDs []uint32, a, b, c unsafe.Pointer) {
-		if run.perr != nil || len(cIDs) == 0 {
+	run := &stagedRun{st: st, r1: r1, nbInputs: nbInputs}
+	hook := func(cIDs []uint32, a, b, c unsafe.Pointer, wIDs []uint32, values unsafe.Pointer) {
+		if run.perr != nil {
+			return
+		}
+		if !run.inputsPut { // the witness wires are solved before the first level
+			if err := st.PutRange(gm.StageWires, 0, run.nbInputs, values); err != nil {
+				run.perr = err
+				return
+			}
+			run.inputsPut = true
+		}
+		if err := st.PutIndexed(gm.StageWires, values, wIDs); err != nil {
+			run.perr = err
+			return
+		}
+		if run.r1 != nil || len(cIDs) == 0 {
 			return
 		}
 		for _, v := range []struct {
@@ -53,13 +75,19 @@ func (pk *ProvingKey) beginStaged(nbConstraints int) (*stagedRun, csolver.Option
 }
 
 // prove is Prove's device block with the staged inputs: the solver ran with
-// beginStaged's option; only the wires are copied afterwards.
+// beginStaged's option, so every wire (and a, b, c) is already on its way to
+// the device.
 func (run *stagedRun) prove(w []fr.Element, r, s *fr.Element, ar, bs, krs unsafe.Pointer) error {
 	if run.perr != nil {
 		return run.perr
 	}
-	if err := run.st.PutRange(gm.StageWires, 0, len(w), unsafe.Pointer(&w[0])); err != nil {
-		return err
+	if !run.inputsPut { // a system without levels: the hook never ran
+		if err := run.st.PutRange(gm.StageWires, 0, len(w), unsafe.Pointer(&w[0])); err != nil {
+			return err
+		}
+	}
+	if run.r1 != nil {
+		return run.st.ProveR1CS(run.r1, unsafe.Pointer(r), unsafe.Pointer(s), ar, bs, krs)
 	}
 	return run.st.Prove(unsafe.Pointer(r), unsafe.Pointer(s), ar, bs, krs)
 }

@@ -323,8 +323,27 @@ def test_levelhook_diff_applies_to_the_reference_solver(tmp_path):
     # the staged prover uses exactly the hook type the patch declares
     staged = open(os.path.join(GO_DIR, "icicle_bn254", "staged.go")).read()
     assert "csolver.WithLevelHook(hook)" in staged
-    assert "func(cIDs []uint32, a, b, c unsafe.Pointer)" in staged and \
-        "type LevelHook func(cIDs []uint32, a, b, c unsafe.Pointer)" in text
+    sig = "func(cIDs []uint32, a, b, c unsafe.Pointer, wIDs []uint32, values unsafe.Pointer)"
+    assert sig in staged and "type LevelHook " + sig in text
+    # every solved wire is logged where solver.set counts it, and each level's
+    # log entries reach the hook (wires staged during Solve, not after it)
+    assert text.count("s.wireLog[n-1-s.nbInputs] = uint32(id)") == 2
+    assert text.count("wIDs := solver.wireLog[solver.logMark:end]") == 2
+    assert "st.PutIndexed(gm.StageWires, values, wIDs)" in staged
+    assert "PutRange(gm.StageWires, 0, len(w)" in staged  # only the no-level fallback
+    # the diff is what tools/make_levelhook_patch.py generates from the reference
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("mk", os.path.join(ROOT, "tools", "make_levelhook_patch.py"))
+    mk = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mk)
+    import difflib
+    regen = []
+    for rel, fn in (("constraint/bn254/solver.go", mk.patch_solver), ("constraint/bls12-377/solver.go",
+                                                                     mk.patch_solver),
+                    ("constraint/solver/options.go", mk.patch_options)):
+        a = open(os.path.join(ref, rel)).read()
+        regen += difflib.unified_diff(a.splitlines(True), fn(a).splitlines(True), "a/" + rel, "b/" + rel, n=3)
+    assert "".join(regen) == text
 
 
 def test_prove_diff_applies_to_the_reference_plonk_prover(tmp_path):

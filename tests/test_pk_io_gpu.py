@@ -156,6 +156,45 @@ def test_staged_inputs_by_level(gm_ctx, oracle, cname, k):
         dpk.free()
 
 
+@pytest.mark.parametrize("reuse", ["1", "0"])
+def test_staged_buffers_reused_across_proofs(gm_ctx, oracle, monkeypatch, reuse):
+    """gm_g16_stage_free parks the stage's buffers with the key and the next
+    gm_g16_stage_begin reuses them (no per-proof allocation): consecutive staged
+    proofs on one key -- whole-vector puts, then per-level puts in another order,
+    then two stages open at once (one reuses the spare, one is fresh) -- all equal
+    the oracle.  GM_G16_STAGE_REUSE=0 gives the same proofs without reuse."""
+    import gnark_mi355x as gm
+    monkeypatch.setenv("GM_G16_STAGE_REUSE", reuse)
+    r1, pk, (W, A, B, C), rb, sb, exp = _setup(oracle, "bn254", 700)
+    nc = len(A) // 32
+    dpk = gm.ProvingKey(gm_ctx, "bn254", pk, r1.domain_size, r1.nb_wires, r1.nb_public)
+
+    def fill(st, order):
+        for lv in np.array_split(order, 9):
+            for which, vec in ((st.A, A), (st.B, B), (st.C, C)):
+                st.put_indexed(which, vec, lv)
+        st.put_range(st.WIRES, 0, W)
+
+    try:
+        for order in (np.arange(nc), np.arange(nc)[::-1].copy(), np.random.default_rng(3).permutation(nc)):
+            st = dpk.stage(nc)
+            try:
+                fill(st, order)
+                assert st.prove(rb, sb) == exp
+            finally:
+                st.free()
+        s1, s2 = dpk.stage(nc), dpk.stage(nc)
+        try:
+            fill(s2, np.arange(nc))
+            fill(s1, np.arange(nc)[::-1].copy())
+            assert s1.prove(rb, sb) == exp and s2.prove(rb, sb) == exp
+        finally:
+            s1.free()
+            s2.free()
+    finally:
+        dpk.free()
+
+
 def test_pk_cache_rejects_corrupt_headers_and_indices(gm_ctx, oracle, tmp_path):
     """gm_g16_pk_load_cache checks the header invariants, the device-layout
     fingerprint and every compaction index against the wire slice (k_gather_fr

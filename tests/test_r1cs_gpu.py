@@ -148,3 +148,52 @@ def test_groth16_prove_r1cs_bsb22(gm_ctx, oracle):
     finally:
         h.free()
         dpk.free()
+
+
+@pytest.mark.parametrize("cname", ["bn254", "bls12377"])
+def test_groth16_stage_prove_r1cs_wires_by_level(gm_ctx, oracle, cname):
+    """gm_g16_stage_prove_r1cs: the wires handed over in pieces while Solve runs
+    (GM_STAGE_WIRES ranges and indexed puts, as the wire-extended level hook of
+    integration/go/solver_levelhook.diff delivers them), a, b, c evaluated from the
+    resident R1CS -- the proof equals the oracle's; twice on one key (the stage
+    buffers are reused), and a system of another size is refused."""
+    import gnark_mi355x as gm
+    c = pyref.CURVES[cname]
+    r1, W = R.squaring_chain(1500 if cname == "bn254" else 400, cname, x=11)
+    tox = R.encode_vec(cname, [t % c.r for t in TOXIC])
+    pk = oracle.g16_setup(cname, r1, tox)
+    a, b, cc = r1.solve_abc(W)
+    enc = lambda v: R.encode_vec(cname, v)
+    rb, sb = enc([0x5555]), enc([0x6666])
+    exp = oracle.g16_prove(cname, pk, r1.nb_public, enc(W), enc(a), enc(b), enc(cc), rb, sb)
+    dpk = gm.ProvingKey(gm_ctx, cname, pk, r1.domain_size, r1.nb_wires, r1.nb_public)
+    h = _upload(gm_ctx, r1)
+    Wb = enc(W)
+    nw = r1.nb_wires
+    try:
+        for rep in range(2):
+            st = dpk.stage(r1.nc)
+            try:
+                rng = np.random.default_rng(rep)
+                st.put_range(st.WIRES, 0, Wb[:32 * r1.nb_public])  # the witness inputs
+                rest = rng.permutation(np.arange(r1.nb_public, nw)) if rep else np.arange(r1.nb_public, nw)
+                for lv in np.array_split(rest, 13):  # "levels" of solved wires
+                    if rep:
+                        st.put_indexed(st.WIRES, Wb, lv)
+                    else:
+                        st.put_range(st.WIRES, int(lv[0]), Wb[32 * int(lv[0]):32 * (int(lv[-1]) + 1)])
+                assert st.prove_r1cs(h, rb, sb) == exp
+            finally:
+                st.free()
+        r2, _ = R.squaring_chain(10, cname)
+        h2 = _upload(gm_ctx, r2)
+        st = dpk.stage(r1.nc)
+        try:
+            with pytest.raises(gm.GmError, match="does not match"):
+                st.prove_r1cs(h2, rb, sb)
+        finally:
+            st.free()
+            h2.free()
+    finally:
+        h.free()
+        dpk.free()
