@@ -171,6 +171,7 @@ int gm_destroy(gm_ctx* ctx) {
   if (ctx->copy) hipStreamSynchronize(ctx->copy);
   for (hipStream_t s : ctx->slot_stream)
     if (s) hipStreamSynchronize(s);
+  if (ctx->g16_stream) hipStreamSynchronize(ctx->g16_stream);
   orphan_pending_msms(ctx);
   ntt_domains_free(ctx);
   for (gm::ArenaState* a : {&ctx->arena, &ctx->slots[0], &ctx->slots[1], &ctx->slots[2]}) {
@@ -186,6 +187,7 @@ int gm_destroy(gm_ctx* ctx) {
   }
   for (hipStream_t s : ctx->slot_stream)
     if (s) hipStreamDestroy(s);
+  if (ctx->g16_stream) hipStreamDestroy(ctx->g16_stream);
   hipStreamDestroy(ctx->stream);
   if (ctx->aux) hipStreamDestroy(ctx->aux);
   if (ctx->copy) hipStreamDestroy(ctx->copy);
@@ -196,6 +198,36 @@ int gm_destroy(gm_ctx* ctx) {
     if (ctx->h2d_ev[i]) hipEventDestroy(ctx->h2d_ev[i]);
   }
   delete ctx;
+  return GM_OK;
+}
+
+int gm_trim(gm_ctx* ctx) {
+  if (!ctx) return GM_ERR_INVALID;
+  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  if (!ctx->live_msms.empty()) {
+    set_error("gm_trim: MSMs are pending on this context (gm_msm_wait them first)");
+    return GM_ERR_INVALID;
+  }
+  GM_HIP(hipSetDevice(ctx->device));
+  GM_HIP(hipStreamSynchronize(ctx->stream));
+  if (ctx->aux) GM_HIP(hipStreamSynchronize(ctx->aux));
+  if (ctx->copy) GM_HIP(hipStreamSynchronize(ctx->copy));
+  for (hipStream_t st : ctx->slot_stream)
+    if (st) GM_HIP(hipStreamSynchronize(st));
+  if (ctx->g16_stream) GM_HIP(hipStreamSynchronize(ctx->g16_stream));
+  for (gm::ArenaState* a : {&ctx->arena, &ctx->slots[0], &ctx->slots[1], &ctx->slots[2]}) {
+    for (auto& ch : a->chunks) hipFree(ch.base);
+    a->chunks.clear();
+    a->cur_chunk = a->cur_top = 0;
+  }
+  if (ctx->in_abc) hipFree(ctx->in_abc);
+  ctx->in_abc = nullptr;
+  ctx->in_abc_cap = 0;
+  for (int i = 0; i < gm_ctx::H2D_SLOTS; i++) {
+    if (ctx->h2d_pin[i]) hipHostFree(ctx->h2d_pin[i]);
+    ctx->h2d_pin[i] = nullptr;
+  }
+  ntt_domains_free(ctx);
   return GM_OK;
 }
 

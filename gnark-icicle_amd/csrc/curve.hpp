@@ -116,7 +116,9 @@ GM_DEV void xyzz_add_aff(XYZZ<F>& a, const Affine<F>& p) {
 // of p (zz * PP with PP != 0 mod p), so fe_is_zero(zz) still tests infinity.
 // The digit sign is applied to S2 = y zzz (carry-free 2p - S2) rather than to y,
 // and X3 = R^2 - PPP - 2Q takes one borrow chain (fe_sub2x_lz).
-template <class P>
+// CH: one dependent mad chain per product (fe_mul CHAIN) -- A/B variant of the
+// accumulation kernel only (GM_MSM_ACC_CHAIN=1).
+template <class P, bool CH = false>
 GM_DEV void xyzz_add_aff_lz(XYZZ<Fe<P>>& a, const Affine<Fe<P>>& p, bool neg) {
   static_assert(P::BITS + 7 <= RADIX * P::N, "lazy reduction needs R' > 128 p");
   using F = Fe<P>;
@@ -128,9 +130,9 @@ GM_DEV void xyzz_add_aff_lz(XYZZ<Fe<P>>& a, const Affine<Fe<P>>& p, bool neg) {
     a.zzz = fe_one<P>();
     return;
   }
-  F Pd = fe_sub_lz<8>(fe_mul_lz(p.x, a.zz), a.x);   // U2 - X1   < 10p
+  F Pd = fe_sub_lz<8>(fe_mul<P, false, CH>(p.x, a.zz), a.x);   // U2 - X1   < 10p
   // +-S2 - Y1 < 6p  (S2 = y zzz < 2p; 2p - S2 in (0, 2p])
-  F R = fe_sub_lz<4>(fe_cneg2p_cf(fe_mul_lz(p.y, a.zzz), neg), a.y);
+  F R = fe_sub_lz<4>(fe_cneg2p_cf(fe_mul<P, false, CH>(p.y, a.zzz), neg), a.y);
   if (fe_is_zero_lz<10>(Pd)) {
     if (fe_is_zero_lz<6>(R)) {
       Affine<F> q = p;
@@ -141,12 +143,12 @@ GM_DEV void xyzz_add_aff_lz(XYZZ<Fe<P>>& a, const Affine<Fe<P>>& p, bool neg) {
     }
     return;
   }
-  F PP = fe_sqr_lz(Pd);                              // < 2p
-  F PPP = fe_mul_lz(Pd, PP);                         // < 2p
-  a.zz = fe_mul_lz(a.zz, PP);
-  F Q = fe_mul_lz(a.x, PP);                          // < 2p
-  a.zzz = fe_mul_lz(a.zzz, PPP);
-  F X3 = fe_sub2x_lz<6>(fe_sqr_lz(R), PPP, Q);       // R^2 - PPP - 2Q + 6p < 8p
+  F PP = fe_sqr<P, false, CH>(Pd);                              // < 2p
+  F PPP = fe_mul<P, false, CH>(Pd, PP);                         // < 2p
+  a.zz = fe_mul<P, false, CH>(a.zz, PP);
+  F Q = fe_mul<P, false, CH>(a.x, PP);                          // < 2p
+  a.zzz = fe_mul<P, false, CH>(a.zzz, PPP);
+  F X3 = fe_sub2x_lz<6>(fe_sqr<P, false, CH>(R), PPP, Q);       // R^2 - PPP - 2Q + 6p < 8p
   // R (< 6p) * (Q - X3 + 9p < 11p) + (5p - Y1) (Y1 < 4p) * PPP (< 2p), ONE unsigned
   // reduction (fe_mul2_redc_u; Y1's negation folded into the carry-free operand
   // 5p - Y1, so no signed columns and no + p pass): < 76 p^2 / R' + p < 1.5p.
@@ -154,9 +156,9 @@ GM_DEV void xyzz_add_aff_lz(XYZZ<Fe<P>>& a, const Affine<Fe<P>>& p, bool neg) {
   // hold it: N (3 + 2 + 1) 2^58 < 2^64 for N <= 10 (BN254; BLS12-377's 13 limbs
   // take the normalised difference)
   if constexpr (P::N <= 10)
-    a.y = fe_mul2_redc_u(R, fe_sub_cf<9>(Q, X3), fe_negk_cf<5>(a.y), PPP);
+    a.y = fe_mul2_redc_u<P, CH>(R, fe_sub_cf<9>(Q, X3), fe_negk_cf<5>(a.y), PPP);
   else
-    a.y = fe_mul2_redc_u(R, fe_sub_lz<8>(Q, X3), fe_negk_cf<5>(a.y), PPP);
+    a.y = fe_mul2_redc_u<P, CH>(R, fe_sub_lz<8>(Q, X3), fe_negk_cf<5>(a.y), PPP);
   a.x = X3;
 }
 // Lazily reduced a += p for G2 buckets (Fp2 coordinates).  Invariants: every

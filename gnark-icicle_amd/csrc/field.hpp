@@ -302,7 +302,7 @@ GM_DEV Fe<P> fe_mul(const Fe<P>& a, const Fe<P>& b) {
 }
 
 // Squaring: the symmetric products a_i a_j (i != j) are formed once and doubled.
-template <class P, bool REDUCE = true>
+template <class P, bool REDUCE = true, bool CHAIN = GM_FE_CHAIN>
 GM_DEV Fe<P> fe_sqr(const Fe<P>& a) {
   constexpr int N = P::N;
   uint32_t m[N];
@@ -310,7 +310,7 @@ GM_DEV Fe<P> fe_sqr(const Fe<P>& a) {
   uint64_t acc = 0;
 #pragma unroll
   for (int k = 0; k < 2 * N - 1; k++) {
-    if constexpr (GM_FE_CHAIN) {
+    if constexpr (CHAIN) {
       if (k) __asm__ volatile("" : "+v"(acc));
     }
     uint64_t cross = 0;
@@ -383,7 +383,7 @@ GM_DEV Fe<P> fe_sqr_lz(const Fe<P>& a) { return fe_sqr<P, false>(a); }
 // lane-pair Fp2 product, whose two lanes then run the same instructions.  Column bound:
 // N (2^58 + 2^59 + 2^58) < 2^64 for N <= 14 with x1, y1, y2 normalised and x2
 // limbs < 2^30.  Output < (x1 y1 + x2 y2) / R' + p, limbs normalised.
-template <class P>
+template <class P, bool CHAIN = GM_FE_CHAIN>
 GM_DEV Fe<P> fe_mul2_redc_u(const Fe<P>& x1, const Fe<P>& y1, const Fe<P>& x2, const Fe<P>& y2) {
   constexpr int N = P::N;
   static_assert(N <= 14, "unsigned two-product column bound");
@@ -392,7 +392,7 @@ GM_DEV Fe<P> fe_mul2_redc_u(const Fe<P>& x1, const Fe<P>& y1, const Fe<P>& x2, c
   uint64_t acc = 0;
 #pragma unroll
   for (int k = 0; k < 2 * N - 1; k++) {
-    if constexpr (GM_FE_CHAIN) {
+    if constexpr (CHAIN) {
       if (k) __asm__ volatile("" : "+v"(acc));
     }
 #pragma unroll

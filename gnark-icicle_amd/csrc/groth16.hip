@@ -249,6 +249,9 @@ int pk_upload_ranges(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsigned f
       largest = std::max(largest, b);
     }
     need += largest / 8;  // gnark-layout staging of the largest array
+    // the streamed (dump) path builds a shared array's compacted precomputed copy
+    // before expanding it: one more array at the upload's peak
+    if (src && (pk->wshare[0] || pk->wshare[1] || pk->wshare[2])) need += largest;
     size_t fr = 0, tot = 0;
     const char* fenv = getenv("GM_PK_PRECOMPUTE_FRAC");
     const double frac = fenv ? atof(fenv) : 0.6;
@@ -547,14 +550,21 @@ struct HostStagedH : HSource {
       if (hipSetDevice(ctx->device) != hipSuccess) r = GM_ERR_DEVICE;
       const void* src[3] = {ha, hb, hc};
       void* dst[3] = {da, db, dc};
-      if (pinned) {
-        for (int i = 0; i < gm_ctx::H2D_SLOTS && r == GM_OK; i++) {
-          if (!ctx->h2d_pin[i] && hipHostMalloc(&ctx->h2d_pin[i], gm_ctx::H2D_SLOT, hipHostMallocDefault) != hipSuccess)
-            r = GM_ERR_OOM;
-          if (r == GM_OK && !ctx->h2d_ev[i] &&
-              hipEventCreateWithFlags(&ctx->h2d_ev[i], hipEventDisableTiming) != hipSuccess)
-            r = GM_ERR_DEVICE;
+      // the ring is created on first use; when pinned memory (or an event) is not
+      // available the copies take the pageable path instead of failing the prove
+      bool ring = pinned;
+      for (int i = 0; i < gm_ctx::H2D_SLOTS && ring && r == GM_OK; i++) {
+        if (!ctx->h2d_pin[i] && hipHostMalloc(&ctx->h2d_pin[i], gm_ctx::H2D_SLOT, hipHostMallocDefault) != hipSuccess) {
+          ctx->h2d_pin[i] = nullptr;
+          ring = false;
         }
+        if (ring && !ctx->h2d_ev[i] && hipEventCreateWithFlags(&ctx->h2d_ev[i], hipEventDisableTiming) != hipSuccess) {
+          ctx->h2d_ev[i] = nullptr;
+          ring = false;
+        }
+      }
+      (void)hipGetLastError();  // a failed allocation above is not the prove's error
+      if (ring) {
         bool used[gm_ctx::H2D_SLOTS] = {};
         int slot = 0;
         for (int k = 0; k < 3 && r == GM_OK; k++)
@@ -898,11 +908,15 @@ int g16_sums_t(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, HSource& hs, G
   // ordered after the plans / gathers: one MSM's bucket reduction (latency-bound,
   // one or two waves per SIMD) then runs beside the next one's accumulation
   // instead of before it.
-  static const bool two = getenv("GM_G16_MSM_STREAMS") && atoi(getenv("GM_G16_MSM_STREAMS")) != 0;
+  // (read per prove: the parity tests flip it).  The stream is the prove's own
+  // (gm_ctx::g16_stream), not an async-MSM slot stream, so a pending
+  // gm_msm_async never serialises the prove's MSMs behind it.
+  const char* two_env = getenv("GM_G16_MSM_STREAMS");
+  const bool two = two_env && atoi(two_env) != 0;
   hipStream_t st1 = st;
   if (two) {
-    if (!ctx->slot_stream[1]) GM_HIP(hipStreamCreateWithFlags(&ctx->slot_stream[1], hipStreamNonBlocking));
-    st1 = ctx->slot_stream[1];
+    if (!ctx->g16_stream) GM_HIP(hipStreamCreateWithFlags(&ctx->g16_stream, hipStreamNonBlocking));
+    st1 = ctx->g16_stream;
     hipEvent_t ev;
     GM_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     const hipError_t e1 = hipEventRecord(ev, st);  // the gathers and the shared plan
@@ -1195,9 +1209,10 @@ int gm_g16_prove(gm_ctx* ctx, gm_g16_pk* pk, const void* wires, const void* a, c
   // a / b / c: the context's input allocation (gm_ctx::in_abc), not the arena
   const size_t abc = 3 * 32 * pk->n;
   if (ctx->in_abc_cap < abc) {
-    if (ctx->in_abc) GM_HIP(hipFree(ctx->in_abc));
-    ctx->in_abc = nullptr;
+    void* old = ctx->in_abc;
+    ctx->in_abc = nullptr;  // released below; never left pointing at freed memory
     ctx->in_abc_cap = 0;
+    if (old) GM_HIP(hipFree(old));
     if (hipMalloc(&ctx->in_abc, abc) != hipSuccess) {
       ctx->in_abc = nullptr;
       set_error("prove: hipMalloc of the a/b/c input buffer failed");

@@ -442,6 +442,7 @@ GM_DEV PackedPt<PW> load_packed_pt(const uint32_t* __restrict__ src) {
 template <class F>
 struct LazyAcc {
   static constexpr bool on = false;
+  template <bool CH = false>
   GM_DEV static void add(XYZZ<F>& a, Affine<F> p, bool neg) {
     if (neg) p.y = fe_neg(p.y);
     xyzz_add_aff(a, p);
@@ -451,12 +452,16 @@ struct LazyAcc {
 template <class P>
 struct LazyAcc<Fe<P>> {
   static constexpr bool on = true;
-  GM_DEV static void add(XYZZ<Fe<P>>& a, const Affine<Fe<P>>& p, bool neg) { xyzz_add_aff_lz(a, p, neg); }
+  template <bool CH = false>
+  GM_DEV static void add(XYZZ<Fe<P>>& a, const Affine<Fe<P>>& p, bool neg) {
+    xyzz_add_aff_lz<P, CH>(a, p, neg);
+  }
   GM_DEV static XYZZ<Fe<P>> canon(const XYZZ<Fe<P>>& a) { return xyzz_canon_lz(a); }
 };
 template <class P, int B>
 struct LazyAcc<Fe2<P, B>> {
   static constexpr bool on = true;
+  template <bool CH = false>
   GM_DEV static void add(XYZZ<Fe2<P, B>>& a, Affine<Fe2<P, B>> p, bool neg) {
     if (neg) p.y = fe_neg(p.y);
     xyzz_add_aff_lz(a, p);
@@ -482,7 +487,7 @@ GM_DEV void accum_emit(uint32_t b, const XYZZ<F>& acc_raw, bool is_first, bool i
 // PREFETCH: the next entry's point words are loaded while this add runs.
 // IDXPF (without PREFETCH): only the next entry's key and value are, so the
 // point address of each iteration is known when it starts.
-template <class F, bool PREFETCH, bool IDXPF = false>
+template <class F, bool PREFETCH, bool IDXPF = false, bool CH = false>
 GM_DEV void accum_seg_body(const uint32_t* __restrict__ points, uint32_t n,
                                                        const uint32_t* __restrict__ keys,
                                                        const uint32_t* __restrict__ vals,
@@ -535,7 +540,7 @@ GM_DEV void accum_seg_body(const uint32_t* __restrict__ points, uint32_t n,
     }
     if (!PREFETCH) P = load_packed_pt<PW>(points + (size_t)(v & 0x7fffffffu) * PW);
     Affine<F> A = load_affine_packed<F>(P.w);
-    LazyAcc<F>::add(acc, A, (v >> 31) != 0);
+    LazyAcc<F>::template add<CH>(acc, A, (v >> 31) != 0);
     if (PREFETCH) {
       v = vn;
       P = Pn;
@@ -563,6 +568,86 @@ k_msm_accum_seg(const uint32_t* __restrict__ points, uint32_t n, const uint32_t*
                 uint32_t K, XYZZ<F>* __restrict__ buckets, XYZZ<F>* __restrict__ part_first,
                 XYZZ<F>* __restrict__ part_last, uint32_t* __restrict__ err) {
   accum_seg_body<F, false>(points, n, keys, vals, offsets, total, K, buckets, part_first, part_last, err);
+}
+// The default G1 body (k_msm_accum_seg_ch): keys and values arrive four entries
+// per 16-byte load instead of one 4-byte load per entry.  A thread's slice is K
+// consecutive entries and consecutive lanes are K entries apart, so each 4-byte
+// load touched one cache line per lane and the line rarely survived in L1 until
+// the lane's next entry (rocprofv3 FETCH_SIZE of the accumulation: 2.8 GB per
+// 2^20 MSM against 1.1 GB of 64-byte point gathers, profiles/r05f_*).  The next
+// group's keys / values are loaded at the last entry of the current group.  (Pinning
+// the point's four 16-byte loads with an empty asm, against the vectoriser's
+// unaligned x2 / x3 / x4 split, costs 32 B of scratch per lane.)  Reads past
+// the thread's last entry stay inside the allocation: slices start at multiples
+// of K (K % 4 == 0) and the workspace arena rounds every allocation to 256 bytes.
+template <class F, bool CH>
+GM_DEV void accum_seg_body_v4(const uint32_t* __restrict__ points, uint32_t n, const uint32_t* __restrict__ keys,
+                              const uint32_t* __restrict__ vals, const uint32_t* __restrict__ offsets,
+                              uint32_t total, uint32_t K, XYZZ<F>* __restrict__ buckets,
+                              XYZZ<F>* __restrict__ part_first, XYZZ<F>* __restrict__ part_last,
+                              uint32_t* __restrict__ err) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t Mv = offsets[total];  // valid (non-zero-digit) entries
+  const uint32_t start = t * K;
+  if (start >= Mv) return;
+  const uint32_t end = min(start + K, Mv);
+  uint4 kg = *reinterpret_cast<const uint4*>(keys + start);
+  uint4 vg = *reinterpret_cast<const uint4*>(vals + start);
+  bool first = true;
+  XYZZ<F> acc = xyzz_inf<F>();
+  uint32_t cur = kg.x;
+  constexpr int PW = 2 * Coord<F>::WORDS;  // u32 words per packed point
+  for (uint32_t q = start; q < end; q++) {
+    const uint32_t k = kg.x, v = vg.x;
+    const uint32_t idx = v & 0x7fffffffu;
+    if (idx >= n) {
+      atomicOr(err, 2u);
+      return;
+    }
+    const PackedPt<PW> P = load_packed_pt<PW>(points + (size_t)idx * PW);
+    // next entry: shift the group; at a group boundary load the next group (its
+    // latency overlaps this entry's add)
+    if (((q - start) & 3) == 3) {
+      if (q + 1 < end) {
+        kg = *reinterpret_cast<const uint4*>(keys + q + 1);
+        vg = *reinterpret_cast<const uint4*>(vals + q + 1);
+      }
+    } else {
+      kg = make_uint4(kg.y, kg.z, kg.w, kg.w);
+      vg = make_uint4(vg.y, vg.z, vg.w, vg.w);
+    }
+    if (k != cur) {
+      accum_emit(cur, acc, first, false, start, end, t, offsets, buckets, part_first, part_last);
+      first = false;
+      acc = xyzz_inf<F>();
+      cur = k;
+    }
+    const Affine<F> A = load_affine_packed<F>(P.w);
+    LazyAcc<F>::template add<CH>(acc, A, (v >> 31) != 0);
+  }
+  accum_emit(cur, acc, first, true, start, end, t, offsets, buckets, part_first, part_last);
+}
+
+// Same with one dependent mad chain per product inside the add (the default for
+// BN254 G1 since r05; GM_MSM_ACC_CHAIN=0 selects k_msm_accum_seg).  Applied to
+// every MSM kernel it slowed the one-to-two-wave reduction kernels (r04h).
+template <class F>
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4)))
+k_msm_accum_seg_ch(const uint32_t* __restrict__ points, uint32_t n, const uint32_t* __restrict__ keys,
+                   const uint32_t* __restrict__ vals, const uint32_t* __restrict__ offsets, uint32_t total,
+                   uint32_t K, XYZZ<F>* __restrict__ buckets, XYZZ<F>* __restrict__ part_first,
+                   XYZZ<F>* __restrict__ part_last, uint32_t* __restrict__ err) {
+  accum_seg_body_v4<F, true>(points, n, keys, vals, offsets, total, K, buckets, part_first, part_last, err);
+}
+// the chain kernel with one 4-byte key / value load per entry (GM_MSM_ACC_V4=0; A/B)
+template <class F>
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4)))
+k_msm_accum_seg_ch1(const uint32_t* __restrict__ points, uint32_t n, const uint32_t* __restrict__ keys,
+                    const uint32_t* __restrict__ vals, const uint32_t* __restrict__ offsets, uint32_t total,
+                    uint32_t K, XYZZ<F>* __restrict__ buckets, XYZZ<F>* __restrict__ part_first,
+                    XYZZ<F>* __restrict__ part_last, uint32_t* __restrict__ err) {
+  accum_seg_body<F, false, false, true>(points, n, keys, vals, offsets, total, K, buckets, part_first, part_last,
+                                        err);
 }
 // Same with the next key / value prefetched (GM_MSM_ACCUM=idx; A-B).
 template <class F>
@@ -1161,6 +1246,14 @@ int msm_launch(gm_ctx* ctx, Arena& arena, const MsmPlan& plan, const void* point
         if constexpr (AccumW4<DF>::ok) {
           if (!prefetch) accum = k_msm_accum_seg<DF>;
           if (ov && !strcmp(ov, "idx")) accum = k_msm_accum_seg_idx<DF>;
+          // default since r05: one mad chain per product in the G1 accumulation only
+          // (115 instead of 127 VGPRs; same box, isolated launch 1.306-1.318 vs
+          // 1.311-1.345 ms at 2^20, Groth16 2^24 within noise,
+          // profiles/r05e_acc_chain_ab.txt); GM_MSM_ACC_CHAIN=0: the split columns
+          static const bool acc_chain = !getenv("GM_MSM_ACC_CHAIN") || atoi(getenv("GM_MSM_ACC_CHAIN")) != 0;
+          static const bool acc_v4 = !getenv("GM_MSM_ACC_V4") || atoi(getenv("GM_MSM_ACC_V4")) != 0;
+          if (acc_chain && !prefetch && !ov)
+            accum = acc_v4 && (t.K & 3) == 0 ? k_msm_accum_seg_ch<DF> : k_msm_accum_seg_ch1<DF>;  // v4: K % 4 == 0
         }
         hipLaunchKernelGGL(accum, dim3(blocks_for(nslices, 128)), dim3(128), 0, st,
                            reinterpret_cast<const uint32_t*>(points_internal), (uint32_t)plan.npts, plan.keys,

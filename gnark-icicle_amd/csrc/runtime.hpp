@@ -83,6 +83,8 @@ struct gm_ctx {
   // the device -- one's sort / reduction (HBM / latency-bound) runs beside
   // another's accumulation (VALU-bound).  Created on first use.
   hipStream_t slot_stream[MSM_SLOTS] = {};
+  // the Groth16 prove's second MSM stream (GM_G16_MSM_STREAMS=1), created on first use
+  hipStream_t g16_stream = nullptr;
   // gm_msm_async handles not yet waited for: gm_destroy drains their device work,
   // releases their slot / readback buffer and orphans them (gm_msm_wait then
   // fails with GM_ERR_INVALID and frees the handle)

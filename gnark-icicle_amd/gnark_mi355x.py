@@ -39,7 +39,7 @@ FR_BYTES = 32
 
 # exported symbols (include/gnark_mi355x.h) -- checked by tests/test_capi_symbols.py
 SYMBOLS = [
-    "gm_last_error", "gm_version", "gm_init", "gm_destroy", "gm_synchronize",
+    "gm_last_error", "gm_version", "gm_init", "gm_destroy", "gm_synchronize", "gm_trim",
     "gm_profile_enable", "gm_profile_reset", "gm_profile_get", "gm_profile_dump",
     "gm_set_msm_window", "gm_set_msm_glv", "gm_malloc", "gm_free", "gm_copy_to_device", "gm_memcpy_h2d",
     "gm_memcpy_d2h", "gm_memcpy_d2d", "gm_copy_points_to_device", "gm_msm", "gm_msm_host_scalars", "gm_points_upload", "gm_msm_prepared", "gm_precompute_layout", "gm_points_upload_precomputed",
@@ -100,6 +100,7 @@ def load_library(path: str = LIB_PATH):
     L.gm_init.argtypes = [i, pvp]
     L.gm_destroy.argtypes = [vp]
     L.gm_synchronize.argtypes = [vp]
+    L.gm_trim.argtypes = [vp]
     L.gm_profile_enable.argtypes = [vp, i]
     L.gm_profile_reset.argtypes = [vp]
     L.gm_profile_get.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64)]
@@ -254,6 +255,10 @@ class Context:
         _check(L.gm_init(device, ctypes.byref(h)))
         self.handle = h
         self.device = device
+
+    def trim(self):
+        """gm_trim: release the memory the context keeps between calls."""
+        _check(load_library().gm_trim(self.handle))
 
     def close(self):
         if self.handle:

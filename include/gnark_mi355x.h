@@ -52,6 +52,14 @@ int gm_device_count(int* count);
 int gm_init(int device, gm_ctx** out);
 int gm_destroy(gm_ctx* ctx);
 int gm_synchronize(gm_ctx* ctx);
+/* Releases the device memory a context keeps for reuse between calls: the
+ * workspace arenas, the a / b / c input buffer of host-input proves (3 n Fr,
+ * 1.5 GB at 2^24), the pinned H2D ring and the cached NTT domain tables.  All
+ * are re-created on demand by the next call that needs them.  Refused
+ * (GM_ERR_INVALID) while gm_msm_async MSMs are pending.  Call it before
+ * uploading a key whose GM_PK_PRECOMPUTE_AUTO decision should see that memory
+ * as free. */
+int gm_trim(gm_ctx* ctx);
 /* Per-kernel timing with HIP events on the context stream (bench/profiling). */
 int gm_profile_enable(gm_ctx* ctx, int on);
 int gm_profile_reset(gm_ctx* ctx);

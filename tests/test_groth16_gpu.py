@@ -323,3 +323,72 @@ def test_groth16_precompute_auto(gm_ctx, oracle, monkeypatch, frac, expect):
         assert dpk.prove(enc(W), enc(a), enc(b), enc(cc), rb, sb) == exp
     finally:
         dpk.free()
+
+
+@pytest.mark.parametrize("precompute", [False, True])
+def test_groth16_second_msm_stream_with_async_msm_pending(gm_ctx, oracle, monkeypatch, precompute):
+    """GM_G16_MSM_STREAMS=1 (the B, B2 and Z MSMs on the prove's own second
+    stream): host-input and device-input proofs equal the oracle's, also while a
+    gm_msm_async MSM is pending on the same context (its slot stream is not the
+    prove's), and that MSM's result is right."""
+    import gnark_mi355x as gm
+    monkeypatch.setenv("GM_G16_MSM_STREAMS", "1")
+    cname = "bn254"
+    c = pyref.CURVES[cname]
+    r1, W = R.squaring_chain(3000, cname, x=6)
+    tox = R.encode_vec(cname, [t % c.r for t in TOXIC])
+    pk = oracle.g16_setup(cname, r1, tox)
+    a, b, cc = r1.solve_abc(W)
+    enc = lambda v: R.encode_vec(cname, v)
+    rb, sb = enc([0x7171]), enc([0x8282])
+    exp = oracle.g16_prove(cname, pk, r1.nb_public, enc(W), enc(a), enc(b), enc(cc), rb, sb)
+    n = 1 << 16
+    S = gm_ctx.random_scalars(cname, n, seed=0x91)
+    K = gm_ctx.random_scalars(cname, n, seed=0x92)
+    P = gm_ctx.batch_mul_base(cname, False, gm.generator(cname), K, n)
+    msm_exp = oracle.msm(cname, False, S.to_host(), P.to_host())
+    dpk = gm.ProvingKey(gm_ctx, cname, pk, r1.domain_size, r1.nb_wires, r1.nb_public, precompute=precompute)
+    try:
+        assert dpk.prove(enc(W), enc(a), enc(b), enc(cc), rb, sb) == exp
+        pend = gm_ctx.msm_async(cname, S, P, n)
+        got = dpk.prove(enc(W), enc(a), enc(b), enc(cc), rb, sb)
+        assert pend.wait()[1] == msm_exp
+        assert got == exp
+    finally:
+        dpk.free()
+        for x in (S, K, P):
+            x.free()
+
+
+def test_gm_trim_releases_and_recreates(gm_ctx, oracle):
+    """gm_trim frees what the context keeps between calls (arenas, the host-input
+    a / b / c buffer, the pinned ring, NTT tables); later calls re-create them and
+    give the same results.  Refused while an async MSM is pending."""
+    import gnark_mi355x as gm
+    cname = "bn254"
+    c = pyref.CURVES[cname]
+    r1, W = R.squaring_chain(1500, cname, x=4)
+    tox = R.encode_vec(cname, [t % c.r for t in TOXIC])
+    pk = oracle.g16_setup(cname, r1, tox)
+    a, b, cc = r1.solve_abc(W)
+    enc = lambda v: R.encode_vec(cname, v)
+    rb, sb = enc([0x1a1a]), enc([0x2b2b])
+    exp = oracle.g16_prove(cname, pk, r1.nb_public, enc(W), enc(a), enc(b), enc(cc), rb, sb)
+    dpk = gm.ProvingKey(gm_ctx, cname, pk, r1.domain_size, r1.nb_wires, r1.nb_public)
+    S = gm_ctx.random_scalars(cname, 5000, seed=0x31)
+    K = gm_ctx.random_scalars(cname, 5000, seed=0x32)
+    P = gm_ctx.batch_mul_base(cname, False, gm.generator(cname), K, 5000)
+    try:
+        assert dpk.prove(enc(W), enc(a), enc(b), enc(cc), rb, sb) == exp
+        gm_ctx.trim()
+        assert dpk.prove(enc(W), enc(a), enc(b), enc(cc), rb, sb) == exp
+        pend = gm_ctx.msm_async(cname, S, P, 5000)
+        with pytest.raises(gm.GmError, match="pending"):
+            gm_ctx.trim()
+        assert pend.wait()[1] == oracle.msm(cname, False, S.to_host(), P.to_host())
+        gm_ctx.trim()
+        assert gm_ctx.msm(cname, S, P, 5000)[1] == oracle.msm(cname, False, S.to_host(), P.to_host())
+    finally:
+        dpk.free()
+        for x in (S, K, P):
+            x.free()
