@@ -580,7 +580,7 @@ k_msm_accum_seg(const uint32_t* __restrict__ points, uint32_t n, const uint32_t*
 // unaligned x2 / x3 / x4 split, costs 32 B of scratch per lane.)  Reads past
 // the thread's last entry stay inside the allocation: slices start at multiples
 // of K (K % 4 == 0) and the workspace arena rounds every allocation to 256 bytes.
-template <class F, bool CH>
+template <class F, bool CH, bool PREFETCH = false>
 GM_DEV void accum_seg_body_v4(const uint32_t* __restrict__ points, uint32_t n, const uint32_t* __restrict__ keys,
                               const uint32_t* __restrict__ vals, const uint32_t* __restrict__ offsets,
                               uint32_t total, uint32_t K, XYZZ<F>* __restrict__ buckets,
@@ -596,15 +596,16 @@ GM_DEV void accum_seg_body_v4(const uint32_t* __restrict__ points, uint32_t n, c
   bool first = true;
   XYZZ<F> acc = xyzz_inf<F>();
   uint32_t cur = kg.x;
+  uint32_t v = vg.x;
+  if ((v & 0x7fffffffu) >= n) {
+    atomicOr(err, 2u);
+    return;
+  }
   constexpr int PW = 2 * Coord<F>::WORDS;  // u32 words per packed point
+  PackedPt<PW> P;
+  if (PREFETCH) P = load_packed_pt<PW>(points + (size_t)(v & 0x7fffffffu) * PW);
   for (uint32_t q = start; q < end; q++) {
-    const uint32_t k = kg.x, v = vg.x;
-    const uint32_t idx = v & 0x7fffffffu;
-    if (idx >= n) {
-      atomicOr(err, 2u);
-      return;
-    }
-    const PackedPt<PW> P = load_packed_pt<PW>(points + (size_t)idx * PW);
+    const uint32_t k = kg.x;
     // next entry: shift the group; at a group boundary load the next group (its
     // latency overlaps this entry's add)
     if (((q - start) & 3) == 3) {
@@ -616,6 +617,16 @@ GM_DEV void accum_seg_body_v4(const uint32_t* __restrict__ points, uint32_t n, c
       kg = make_uint4(kg.y, kg.z, kg.w, kg.w);
       vg = make_uint4(vg.y, vg.z, vg.w, vg.w);
     }
+    const uint32_t vn = vg.x;  // entry q + 1 (when q + 1 < end)
+    PackedPt<PW> Pn;
+    if (q + 1 < end) {
+      if ((vn & 0x7fffffffu) >= n) {
+        atomicOr(err, 2u);
+        return;
+      }
+      if (PREFETCH) Pn = load_packed_pt<PW>(points + (size_t)(vn & 0x7fffffffu) * PW);
+    }
+    if (!PREFETCH) P = load_packed_pt<PW>(points + (size_t)(v & 0x7fffffffu) * PW);
     if (k != cur) {
       accum_emit(cur, acc, first, false, start, end, t, offsets, buckets, part_first, part_last);
       first = false;
@@ -624,6 +635,8 @@ GM_DEV void accum_seg_body_v4(const uint32_t* __restrict__ points, uint32_t n, c
     }
     const Affine<F> A = load_affine_packed<F>(P.w);
     LazyAcc<F>::template add<CH>(acc, A, (v >> 31) != 0);
+    v = vn;
+    if (PREFETCH) P = Pn;
   }
   accum_emit(cur, acc, first, true, start, end, t, offsets, buckets, part_first, part_last);
 }
@@ -670,6 +683,19 @@ struct AccumW4<Fe<P>> {
 };
 // The next point prefetched into registers while the current add runs (three
 // waves per SIMD for BN254 G1, two for BLS12-377 G1).
+// The prefetching kernel with keys / values in groups of four (default for the
+// prefetching kernel when K % 4 == 0; GM_MSM_ACC_V4=0: k_msm_accum_seg_pf).
+template <class F>
+__global__ void __launch_bounds__(128) k_msm_accum_seg_pf4(const uint32_t* __restrict__ points, uint32_t n,
+                                                           const uint32_t* __restrict__ keys,
+                                                           const uint32_t* __restrict__ vals,
+                                                           const uint32_t* __restrict__ offsets, uint32_t total,
+                                                           uint32_t K, XYZZ<F>* __restrict__ buckets,
+                                                           XYZZ<F>* __restrict__ part_first,
+                                                           XYZZ<F>* __restrict__ part_last,
+                                                           uint32_t* __restrict__ err) {
+  accum_seg_body_v4<F, false, true>(points, n, keys, vals, offsets, total, K, buckets, part_first, part_last, err);
+}
 template <class F>
 __global__ void __launch_bounds__(128) k_msm_accum_seg_pf(const uint32_t* __restrict__ points, uint32_t n,
                                                           const uint32_t* __restrict__ keys,
@@ -707,13 +733,20 @@ struct PairSel<Fe2<P, B>> {
   // 2^22 accumulation 46.1 -> 44.2 ms, profiles/r03i_ab.txt).  GM_MSM_PAIR_PF=0/1
   // overrides.
   // GM_MSM_PAIR_WPE=3 (A/B): BN254 without prefetch capped at three waves.
-  static auto kernel() {
+  // keys / values in groups of four (V4, as the G1 accumulation; needs K % 4 == 0):
+  // default on, GM_MSM_ACC_V4=0 off.
+  static auto kernel(uint32_t K) {
     static const char* pf = getenv("GM_MSM_PAIR_PF");
     static const char* wpe = getenv("GM_MSM_PAIR_WPE");
+    static const bool v4env = !getenv("GM_MSM_ACC_V4") || atoi(getenv("GM_MSM_ACC_V4")) != 0;
+    const bool v4 = v4env && (K & 3) == 0;
     const bool on = pf ? pf[0] != '0' : P::N <= 9;
     if constexpr (P::N <= 9) {
       if (wpe && wpe[0] == '3') return k_msm_accum_seg_pair<P, B, false, 3>;
     }
+    if (v4)
+      return on ? k_msm_accum_seg_pair<P, B, true, GM_PAIR_WPE, true>
+                : k_msm_accum_seg_pair<P, B, false, GM_PAIR_WPE, true>;
     return on ? k_msm_accum_seg_pair<P, B, true> : k_msm_accum_seg_pair<P, B, false>;
   }
   static constexpr auto fixup() { return k_msm_fixup_pair<P, B>; }
@@ -1232,7 +1265,7 @@ int msm_launch(gm_ctx* ctx, Arena& arena, const MsmPlan& plan, const void* point
     const bool prefetch = ov && !strcmp(ov, "prefetch");
     if constexpr (PairSel<DF>::ok) {
       if (pair) {
-        hipLaunchKernelGGL(PairSel<DF>::kernel(), dim3(blocks_for(2 * nslices, 128)), dim3(128), 0, st,
+        hipLaunchKernelGGL(PairSel<DF>::kernel(t.K), dim3(blocks_for(2 * nslices, 128)), dim3(128), 0, st,
                            reinterpret_cast<const uint32_t*>(points_internal), (uint32_t)plan.npts, plan.keys,
                            plan.vals, plan.offsets, t.total, t.K, buckets.as<uint32_t>(), pfirst.as<uint32_t>(),
                            plast.as<uint32_t>(), errw.as<uint32_t>());
@@ -1242,7 +1275,10 @@ int msm_launch(gm_ctx* ctx, Arena& arena, const MsmPlan& plan, const void* point
     }
     if constexpr (kOneLane<DF>) {
       if (!pair) {
+        static const bool acc_v4 = !getenv("GM_MSM_ACC_V4") || atoi(getenv("GM_MSM_ACC_V4")) != 0;
+        const bool v4 = acc_v4 && (t.K & 3) == 0;
         auto accum = prefetch ? k_msm_accum_seg_pf<DF> : (G2 ? k_msm_accum_seg_g2<DF> : k_msm_accum_seg_pf<DF>);
+        if (!G2 && v4 && !ov) accum = k_msm_accum_seg_pf4<DF>;
         if constexpr (AccumW4<DF>::ok) {
           if (!prefetch) accum = k_msm_accum_seg<DF>;
           if (ov && !strcmp(ov, "idx")) accum = k_msm_accum_seg_idx<DF>;
@@ -1251,9 +1287,8 @@ int msm_launch(gm_ctx* ctx, Arena& arena, const MsmPlan& plan, const void* point
           // 1.311-1.345 ms at 2^20, Groth16 2^24 within noise,
           // profiles/r05e_acc_chain_ab.txt); GM_MSM_ACC_CHAIN=0: the split columns
           static const bool acc_chain = !getenv("GM_MSM_ACC_CHAIN") || atoi(getenv("GM_MSM_ACC_CHAIN")) != 0;
-          static const bool acc_v4 = !getenv("GM_MSM_ACC_V4") || atoi(getenv("GM_MSM_ACC_V4")) != 0;
           if (acc_chain && !prefetch && !ov)
-            accum = acc_v4 && (t.K & 3) == 0 ? k_msm_accum_seg_ch<DF> : k_msm_accum_seg_ch1<DF>;  // v4: K % 4 == 0
+            accum = v4 ? k_msm_accum_seg_ch<DF> : k_msm_accum_seg_ch1<DF>;  // v4: K % 4 == 0
         }
         hipLaunchKernelGGL(accum, dim3(blocks_for(nslices, 128)), dim3(128), 0, st,
                            reinterpret_cast<const uint32_t*>(points_internal), (uint32_t)plan.npts, plan.keys,

@@ -284,7 +284,7 @@ GM_DEV PairPt<P> pair_load_pt(const uint32_t* __restrict__ pt) {
 // PF: prefetch the next point's components (2 x NG registers) while the
 // current add runs; without it the other waves hide the load (GM_MSM_PAIR_PF=0).
 // WPE: waves-per-SIMD floor for the register allocator (1 = no cap).
-template <class P, int BETA, bool PF = true, int WPE = GM_PAIR_WPE>
+template <class P, int BETA, bool PF = true, int WPE = GM_PAIR_WPE, bool V4 = false>
 __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_msm_accum_seg_pair(const uint32_t* __restrict__ points, uint32_t n,
                                                             const uint32_t* __restrict__ keys,
@@ -309,8 +309,20 @@ k_msm_accum_seg_pair(const uint32_t* __restrict__ points, uint32_t n,
       if (is_last) pair_emit<P>(part_last + (size_t)t * XW, acc);
     }
   };
-  uint32_t v = vals[start];
-  uint32_t cur = keys[start];
+  // keys / values in 16-byte groups of four entries (as accum_seg_body_v4: one
+  // load per four entries instead of a strided 4-byte load per entry; slices
+  // start at multiples of K, K % 4 == 0 for V4, reads stay in the arena's
+  // 256-byte-rounded allocation)
+  uint4 kg, vg;
+  if constexpr (V4) {
+    kg = *reinterpret_cast<const uint4*>(keys + start);
+    vg = *reinterpret_cast<const uint4*>(vals + start);
+  } else {
+    kg.x = keys[start];
+    vg.x = vals[start];
+  }
+  uint32_t v = vg.x;
+  uint32_t cur = kg.x;
   bool first = true;
   PXYZZ<P> acc = pxyzz_inf<P>();
   if ((v & 0x7fffffffu) >= n) {
@@ -319,12 +331,26 @@ k_msm_accum_seg_pair(const uint32_t* __restrict__ points, uint32_t n,
   }
   PairPt<P> pt = pair_load_pt<P>(points + (size_t)(v & 0x7fffffffu) * 4 * P::NG);
   for (uint32_t q = start; q < end; q++) {
-    const uint32_t k = keys[q];
+    uint32_t k;
+    if constexpr (V4) {
+      k = kg.x;
+      if (((q - start) & 3) == 3) {
+        if (q + 1 < end) {
+          kg = *reinterpret_cast<const uint4*>(keys + q + 1);
+          vg = *reinterpret_cast<const uint4*>(vals + q + 1);
+        }
+      } else {
+        kg = make_uint4(kg.y, kg.z, kg.w, kg.w);
+        vg = make_uint4(vg.y, vg.z, vg.w, vg.w);
+      }
+    } else {
+      k = keys[q];
+    }
     // prefetch the next point's components while this add runs
     uint32_t vn = 0;
     PairPt<P> ptn;
     if (q + 1 < end) {
-      vn = vals[q + 1];
+      vn = V4 ? vg.x : vals[q + 1];
       if ((vn & 0x7fffffffu) >= n) {
         if (!pair_odd()) atomicOr(err, 2u);
         return;
