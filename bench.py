@@ -45,8 +45,9 @@ G16_BYTES_PER_ELEM = 4 * 96 + 160 + 7 * 64 + 128
 # committed rocprofv3 --pmc summaries the roofline's traffic / valu fields are
 # read from (collected by tools/gpu_pmc.sh / tools/pmc_traffic.py on the bench's
 # own MSM workload; NOT measured inside this run)
-PMC_TRAFFIC_FILE = "profiles/r04g_pmc_traffic.json"
-PMC_VALU_FILE = "profiles/r04g_pmc_valu.json"
+PMC_TRAFFIC_FILE = "profiles/r05j_pmc_traffic.json"
+PMC_VALU_FILE = "profiles/r05j_pmc_valu.json"
+ACCUM_KERNEL = "k_msm_accum_seg_ch"  # the default BN254 G1 accumulation (msm_impl.hpp)
 
 
 def parse():
@@ -70,12 +71,21 @@ def parse():
 
 
 def load_pmc_traffic(name):
-    """HBM bytes per launch from a committed rocprofv3 --pmc summary (or None)."""
+    """Fabric bytes per launch of kernel `name` from a committed rocprofv3 --pmc
+    summary (tools/pmc_traffic.py), or None: (gather-calibrated bytes, streaming-
+    corrected bytes).  FETCH_SIZE tallies 64-byte random gathers 1:1 and
+    16-byte-per-lane streaming reads at half their bytes (the calibration in
+    profiles/r05f_gather_fetch_calibration.txt), so the accumulation's traffic --
+    64-byte point gathers plus 16-byte key / value groups -- lies between
+    1024 * FETCH + WRITE and 2 * 1024 * FETCH + WRITE."""
     p = os.path.join(ROOT, PMC_TRAFFIC_FILE)
     try:
         with open(p) as f:
-            return json.load(f).get(name)
-    except (OSError, ValueError):
+            meta = json.load(f)["_meta"]
+        fk = next(v for k, v in meta["fetch_kib"].items() if k == name)
+        wk = meta["write_kib"].get(name, 0.0)
+        return int(1024 * (fk + wk)), int(1024 * (2 * fk + wk))
+    except (OSError, ValueError, KeyError, StopIteration):
         return None
 
 
@@ -211,16 +221,20 @@ def main():
     windows = -(-128 // c) if glv else -(-255 // c)  # ceil((bits + 1) / c), bits = 127 / 254
     mads = npts * windows * MADS_PER_MIXED_ADD      # ~one XYZZ mixed add per (point, window)
     tmads = mads / (acc_avg_ms * 1e-3) / 1e12 if acc_avg_ms > 0 else 0.0
+    traffic = load_pmc_traffic(ACCUM_KERNEL)
     roofline = {
-        "kernel": "k_msm_accum_seg<Fe<Bn254Fp>> (msm_accum_g1)",
+        "kernel": ACCUM_KERNEL + "<Fe<Bn254Fp>> (msm_accum_g1)",
         "bound": "hbm",
         "achieved": round(achieved_gbs, 2),
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
         "frac": round(achieved_gbs / HBM_PEAK_GBS, 5),
-        "traffic": load_pmc_traffic("k_msm_accum_seg"),
+        "traffic": traffic[0] if traffic else None,
+        "traffic_streaming_corrected": traffic[1] if traffic else None,
         "traffic_source": PMC_TRAFFIC_FILE + " (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this MSM "
-                          "workload, 2 x FETCH + WRITE per launch; committed profile, not measured in this run)",
+                          "workload, per launch; traffic = FETCH (64-B gathers are tallied 1:1, calibrated) + WRITE, "
+                          "traffic_streaming_corrected = 2 x FETCH + WRITE (the guide's streaming factor); committed "
+                          "profile of this kernel, not measured in this run)",
         "avg_launch_ms": round(acc_avg_ms, 4),
         "bytes_per_launch": alg_bytes,
         "int_alu": {"achieved": round(tmads, 3), "peak": round(MAD_PEAK_T, 2), "unit": "T v_mad_u64_u32/s",
@@ -235,11 +249,11 @@ def main():
                       "frac": round(alg_bytes / (iso_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
                       "int_alu_frac": round(mads / (iso_avg_ms * 1e-3) / 1e12 / MAD_PEAK_T, 4)}
                      if iso_avg_ms > 0 else None),
-        "valu": load_pmc_valu("k_msm_accum_seg<Fe<Bn254Fp> >"),
+        "valu": load_pmc_valu(ACCUM_KERNEL + "<Fe<Bn254Fp> >"),
         "valu_source": PMC_VALU_FILE + " (rocprofv3 --pmc SQ_* passes; committed profile, not measured in this run)",
         "note": "bound=hbm is the bench contract's roofline for this non-MFMA path; the kernel is NOT HBM-bound: "
-                "its binding resource is VALU issue -- rocprofv3 PMC (" + PMC_VALU_FILE + ") shows VALUBusy "
-                "~0.87 (gfx9 formula, 4 cycles/instr) for k_msm_accum_seg, ~2510 VALU instructions per mixed add; "
+                "its binding resource is VALU issue -- rocprofv3 PMC (" + PMC_VALU_FILE + ", the 'valu' field) "
+                "gives its VALUBusy and VALU instructions per wave (32 entries = 32 mixed adds per thread); "
                 "int_alu prices the v_mad_u64_u32 work at the measured mad-only issue peak (DESIGN.md section 3)",
     }
     kernel_ms = {k: round(v[0] / max(v[1], 1), 4) for k, v in stats.items()}

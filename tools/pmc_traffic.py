@@ -54,7 +54,10 @@ def main():
     for k in sorted(set(fetch) | set(write)):
         res[k] = int(2 * 1024 * fetch.get(k, 0.0) + 1024 * write.get(k, 0.0))
     res["_meta"] = {"fetch_kib": fetch, "write_kib": write,
-                    "correction": "bytes = 2 * 1024 * FETCH_SIZE + 1024 * WRITE_SIZE (gfx950 FETCH_SIZE halving)"}
+                    "correction": "bytes = 2 * 1024 * FETCH_SIZE + 1024 * WRITE_SIZE (gfx950 FETCH_SIZE halving "
+                                  "of 16-B-per-lane streaming reads); 64-byte random gathers are tallied 1:1 "
+                                  "(profiles/r05f_gather_fetch_calibration.txt), so for a gather-dominated "
+                                  "kernel 1024 * FETCH_SIZE is the closer byte count"}
     s = json.dumps(res, indent=1, sort_keys=True)
     if out_path:
         with open(out_path, "w") as f:
