@@ -515,9 +515,10 @@ struct DeviceH : HSource {
 
 // a, b, c in host memory: a helper thread copies them on the context's copy
 // stream (pageable hipMemcpyAsync runs at ~56 GB/s on the box but blocks the
-// calling thread) while the main thread runs the A/B/K MSMs; computeH is
-// launched on the auxiliary stream at the first poll() after the copies are
-// queued.  `after_h` (multi-device) runs right after the launch.
+// calling thread) while the main thread runs the A/B/K MSMs; each vector's
+// computeH chain is launched on the auxiliary stream at the first poll() after
+// that vector's copies are queued, the fused tail once all three are.  `after_h`
+// (multi-device) runs right after the tail is queued.
 template <class C>
 struct HostStagedH : HSource {
   gm_ctx* ctx;
@@ -525,26 +526,50 @@ struct HostStagedH : HSource {
   void *da, *db, *dc;
   const void *ha, *hb, *hc;
   size_t nc;
-  EventPair ev;  // a: copies done (copy stream), b: h ready
+  EventPair ev;             // b: h ready
+  hipEvent_t vev[3] = {};   // a / b / c copied (copy stream)
   std::thread th;
-  std::atomic<bool> queued{false};
+  std::atomic<int> nq{0};   // vectors whose copies are queued (vev recorded)
   std::atomic<int> copy_rc{GM_OK};
   std::string copy_err;
+  int chained = 0;          // computeH chains queued (a, b, c in order)
   bool launched = false;
   std::function<int()> after_h;
   HostStagedH(gm_ctx* x, gm_g16_pk* k, void* a_, void* b_, void* c_, const void* ha_, const void* hb_,
               const void* hc_, size_t n_)
       : ctx(x), pk(k), da(a_), db(b_), dc(c_), ha(ha_), hb(hb_), hc(hc_), nc(n_) {}
+  // memcpy split over `nt` threads (the ring's host-side fill: one thread copies
+  // pageable memory at ~21 GB/s, slower than the DMA behind it)
+  static void par_memcpy(void* dst, const void* src, size_t len, int nt) {
+    if (nt <= 1 || len < (size_t(4) << 20)) {
+      memcpy(dst, src, len);
+      return;
+    }
+    const size_t part = (len / nt + 4095) & ~size_t(4095);
+    std::vector<std::thread> ws;
+    for (int i = 1; i < nt && (size_t)i * part < len; i++) {
+      const size_t o = (size_t)i * part;
+      ws.emplace_back([=] { memcpy((char*)dst + o, (const char*)src + o, std::min(part, len - o)); });
+    }
+    memcpy(dst, src, std::min(part, len));
+    for (auto& w : ws) w.join();
+  }
   int start() {
     int rc;
     if ((rc = ev.create())) return rc;
+    for (hipEvent_t& e : vev) GM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     // GM_G16_H2D_PINNED=0: plain pageable copies (A/B).  A pageable copy issued
     // from this thread while the MSMs ran could stall until an accumulation kernel
     // ended (fresh process: copies after the B2 MSM, 2^24 prove 199 ms instead of
     // ~167, profiles/r04s_g16_host_slow_copies.txt); through the context's pinned
     // ring (memcpy into a 32 MiB slot, then an async copy from pinned memory) the
-    // DMA does not wait for the kernels.
+    // DMA does not wait for the kernels.  The slot fill is split over
+    // GM_G16_H2D_THREADS (4) threads: with one, a 32 MiB fill took 1.55 ms against
+    // the DMA's 0.59 ms and a, b, c arrived only ~75 ms into a 2^24 prove
+    // (profiles/r05i_host_prove_timeline.txt).
     static const bool pinned = !getenv("GM_G16_H2D_PINNED") || atoi(getenv("GM_G16_H2D_PINNED")) != 0;
+    static const int fill_threads =
+        getenv("GM_G16_H2D_THREADS") ? std::max(1, std::min(16, atoi(getenv("GM_G16_H2D_THREADS")))) : 4;
     th = std::thread([this] {
       int r = GM_OK;
       if (hipSetDevice(ctx->device) != hipSuccess) r = GM_ERR_DEVICE;
@@ -564,15 +589,15 @@ struct HostStagedH : HSource {
         }
       }
       (void)hipGetLastError();  // a failed allocation above is not the prove's error
-      if (ring) {
-        bool used[gm_ctx::H2D_SLOTS] = {};
-        int slot = 0;
-        for (int k = 0; k < 3 && r == GM_OK; k++)
+      bool used[gm_ctx::H2D_SLOTS] = {};
+      int slot = 0;
+      for (int k = 0; k < 3 && r == GM_OK; k++) {
+        if (ring) {
           for (size_t off = 0; off < 32 * nc && r == GM_OK; off += gm_ctx::H2D_SLOT) {
             const size_t len = std::min(gm_ctx::H2D_SLOT, 32 * nc - off);
             if (used[slot] && hipEventSynchronize(ctx->h2d_ev[slot]) != hipSuccess) r = GM_ERR_DEVICE;
             if (r) break;
-            memcpy(ctx->h2d_pin[slot], (const char*)src[k] + off, len);
+            par_memcpy(ctx->h2d_pin[slot], (const char*)src[k] + off, len, fill_threads);
             if (hipMemcpyAsync((char*)dst[k] + off, ctx->h2d_pin[slot], len, hipMemcpyHostToDevice, ctx->copy) !=
                     hipSuccess ||
                 hipEventRecord(ctx->h2d_ev[slot], ctx->copy) != hipSuccess)
@@ -580,29 +605,49 @@ struct HostStagedH : HSource {
             used[slot] = true;
             slot = (slot + 1) % gm_ctx::H2D_SLOTS;
           }
-      } else {
-        for (int k = 0; k < 3 && r == GM_OK; k++)
-          if (nc && hipMemcpyAsync(dst[k], src[k], 32 * nc, hipMemcpyHostToDevice, ctx->copy) != hipSuccess)
-            r = GM_ERR_DEVICE;
+        } else if (nc && hipMemcpyAsync(dst[k], src[k], 32 * nc, hipMemcpyHostToDevice, ctx->copy) != hipSuccess) {
+          r = GM_ERR_DEVICE;
+        }
+        if (r == GM_OK && hipEventRecord(vev[k], ctx->copy) != hipSuccess) r = GM_ERR_DEVICE;
+        if (r == GM_OK) nq = k + 1;  // vector k may be chained
       }
-      if (r == GM_OK && hipEventRecord(ev.a, ctx->copy) != hipSuccess) r = GM_ERR_DEVICE;
       if (r) copy_err = "staged a/b/c upload failed";
       copy_rc = r;
-      queued = true;
     });
     return GM_OK;
   }
+  // computeH in pieces as the inputs arrive: the chain of vector k (pad, INTT,
+  // coset NTT) waits only for k's copies, the fused tail for all three
+  // (launch_compute_h's stream choice: ctx->aux, or the main stream with
+  // GM_G16_OVERLAP=0).  block: wait for every copy to be queued.
   int launch(bool block) {
     if (launched) return GM_OK;
-    if (!block && !queued.load()) return GM_OK;
-    if (th.joinable()) th.join();
+    if (block && th.joinable()) th.join();
     if (copy_rc) {
+      if (th.joinable()) th.join();
       set_error(copy_err);
       return copy_rc;
     }
+    // GM_G16_H_INCREMENTAL=0: no chain before all three vectors are queued (A/B)
+    static const bool incremental = !getenv("GM_G16_H_INCREMENTAL") || atoi(getenv("GM_G16_H_INCREMENTAL")) != 0;
+    int q = nq.load();
+    if (!incremental && q < 3) q = 0;
+    if (chained >= q && !(block && q == 3)) return GM_OK;
+    static const bool overlap = !getenv("GM_G16_OVERLAP") || atoi(getenv("GM_G16_OVERLAP")) != 0;
+    const hipStream_t hst = overlap ? ctx->aux : ctx->stream;
+    void* vec[3] = {da, db, dc};
+    {
+      StreamSwap sw(ctx, hst);
+      for (; chained < q; chained++) {
+        GM_HIP(hipStreamWaitEvent(hst, vev[chained], 0));
+        if (int rc = compute_h_chain<C>(ctx, vec[chained], nc, pk->n)) return rc;
+      }
+      if (chained < 3) return GM_OK;
+      if (int rc = compute_h_finish<C>(ctx, da, db, dc, pk->n)) return rc;
+      GM_HIP(hipEventRecord(ev.b, hst));
+    }
     launched = true;
-    int rc = launch_compute_h<C>(ctx, da, db, dc, nc, pk->n, ev.a, ev.b);
-    if (rc) return rc;
+    if (th.joinable()) th.join();
     return after_h ? after_h() : GM_OK;
   }
   int poll() override { return launch(false); }
@@ -617,6 +662,9 @@ struct HostStagedH : HSource {
     if (th.joinable()) th.join();
     hipStreamSynchronize(ctx->copy);
     hipStreamSynchronize(ctx->aux);
+    hipStreamSynchronize(ctx->stream);
+    for (hipEvent_t e : vev)
+      if (e) hipEventDestroy(e);
   }
 };
 

@@ -1,6 +1,6 @@
 #!/bin/bash
-# r05i: copy + kernel trace of 2^24 host-input proves (plain key), then the v4 A/B
-# of every accumulation kernel (tools/gpu_r05h.sh).
+# r05i: copy + kernel trace of 2^24 host-input proves (plain key), the kernel stats of the
+# default bench line, then the counters of the final kernels.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=gpurun_out/r05i; mkdir -p $O && export TMPDIR=/tmp
@@ -9,7 +9,9 @@ cat $O/trace.out
 python3 tools/g16_copy_timeline.py $(ls $O/tr/*kernel_trace.csv $O/tr/*/*kernel_trace.csv 2>/dev/null | head -1) $(ls $O/tr/*memory_copy_trace.csv $O/tr/*/*memory_copy_trace.csv 2>/dev/null | head -1) > $O/host_prove_timeline.txt || exit 1
 head -40 $O/host_prove_timeline.txt
 find $O -name "*.csv" -delete
-bash tools/gpu_r05h.sh
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r05j_prof -o prof -- python3 bench.py --no-cpu-baseline --no-secondary > gpurun_out/r05j_profbench.json 2> gpurun_out/r05j_prof.err || { tail -30 gpurun_out/r05j_prof.err; exit 1; }
+python3 tools/prof_summary.py $(ls gpurun_out/r05j_prof/*kernel_stats.csv gpurun_out/r05j_prof/*/*kernel_stats.csv 2>/dev/null | head -1) > gpurun_out/r05j_rocprof_summary.txt && head -8 gpurun_out/r05j_rocprof_summary.txt
+find gpurun_out/r05j_prof -name "*kernel_trace.csv" -delete
 # counters of the final kernels (r05j): VALU passes over the 2^20 G1 MSM, the 2^20 G2
 # MSM and the 2^24 NTT; FETCH / WRITE over the G1 MSM
 T=r05j
