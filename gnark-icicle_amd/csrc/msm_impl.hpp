@@ -364,6 +364,45 @@ __global__ void __launch_bounds__(256) k_msm_convert_points_glv(const uint32_t* 
   store_affine_packed<F>(dst + (n + i) * PW, a);
 }
 
+// The same conversion with coalesced HBM traffic: a block stages its 256 points
+// through LDS (16-B lane loads / stores over contiguous bytes) and converts
+// from there, instead of each lane reading and writing 64 B at a 64-B lane
+// stride.  GLV: the phi copy goes out through the same LDS tile.  LDS rows are
+// padded by 16 B (point stride Q + 1 uint4) against bank conflicts.
+template <class F, bool GLV>
+__global__ void __launch_bounds__(256) k_msm_convert_points_lds(const uint32_t* __restrict__ src, size_t n,
+                                                                uint32_t* __restrict__ dst) {
+  constexpr int PW = 2 * Coord<F>::WORDS;
+  constexpr uint32_t Q = PW / 4;  // uint4 per point
+  static_assert(PW % 4 == 0, "points are whole uint4s");
+  __shared__ uint4 tile[256 * (Q + 1)];
+  const size_t b0 = (size_t)blockIdx.x * 256;
+  const uint32_t np = (uint32_t)min((size_t)256, n - b0);
+  const uint32_t t = threadIdx.x;
+  const uint4* s = reinterpret_cast<const uint4*>(src) + b0 * Q;
+  for (uint32_t q = t; q < np * Q; q += 256) tile[(q / Q) * (Q + 1) + q % Q] = s[q];
+  __syncthreads();
+  uint32_t* mine = reinterpret_cast<uint32_t*>(tile + t * (Q + 1));
+  Affine<F> a;
+  if (t < np) {
+    a = load_affine_gnark<F>(mine);
+    store_affine_packed<F>(mine, a);
+  }
+  __syncthreads();
+  uint4* d = reinterpret_cast<uint4*>(dst) + b0 * Q;
+  for (uint32_t q = t; q < np * Q; q += 256) d[q] = tile[(q / Q) * (Q + 1) + q % Q];
+  if constexpr (GLV) {
+    __syncthreads();
+    if (t < np) {
+      a.x = glv_phi_x(a.x);
+      store_affine_packed<F>(mine, a);
+    }
+    __syncthreads();
+    uint4* d2 = reinterpret_cast<uint4*>(dst) + (n + b0) * Q;
+    for (uint32_t q = t; q < np * Q; q += 256) d2[q] = tile[(q / Q) * (Q + 1) + q % Q];
+  }
+}
+
 // ---------------------------------------------------------------------------
 // points: gnark layout -> internal layout (once per MSM, into workspace)
 // ---------------------------------------------------------------------------
@@ -1443,14 +1482,26 @@ int msm_device_launch(gm_ctx* ctx, Arena& arena, const void* scalars_dev, const 
     glv = Glv<C>::ok && msm_glv_on(ctx, G2, n);
     if ((rc = ipts.alloc(arena, 2 * Coord<DF>::WORDS * sizeof(uint32_t) * n * (glv ? 2 : 1)))) return rc;
     ProfScope ps(ctx, "msm_convert_points");
-    if constexpr (Glv<C>::ok) {
+    // GM_MSM_CONVERT_LDS=0: the per-lane 64-B conversion kernels (A/B)
+    static const bool lds = !getenv("GM_MSM_CONVERT_LDS") || atoi(getenv("GM_MSM_CONVERT_LDS")) != 0;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(points_dev);
+    if (lds) {
       if (glv)
-        hipLaunchKernelGGL(k_msm_convert_points_glv<DF>, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream,
-                           reinterpret_cast<const uint32_t*>(points_dev), n, ipts.as<uint32_t>());
+        hipLaunchKernelGGL((k_msm_convert_points_lds<DF, true>), dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream,
+                           src, n, ipts.as<uint32_t>());
+      else
+        hipLaunchKernelGGL((k_msm_convert_points_lds<DF, false>), dim3(blocks_for(n, 256)), dim3(256), 0,
+                           ctx->stream, src, n, ipts.as<uint32_t>());
+    } else {
+      if constexpr (Glv<C>::ok) {
+        if (glv)
+          hipLaunchKernelGGL(k_msm_convert_points_glv<DF>, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream, src,
+                             n, ipts.as<uint32_t>());
+      }
+      if (!glv)
+        hipLaunchKernelGGL(k_msm_convert_points<DF>, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream, src, n,
+                           ipts.as<uint32_t>());
     }
-    if (!glv)
-      hipLaunchKernelGGL(k_msm_convert_points<DF>, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream,
-                         reinterpret_cast<const uint32_t*>(points_dev), n, ipts.as<uint32_t>());
     pts = ipts.p;
   }
   MsmPlan plan;
