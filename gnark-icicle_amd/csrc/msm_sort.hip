@@ -92,6 +92,59 @@ static __global__ void __launch_bounds__(1024) k_msm_s1_scatter(const uint32_t* 
   }
 }
 
+// The same partition with coalesced writes: the block's entries are first
+// sorted by bin into an LDS stage (rank + the bin's local base), then written out
+// in stage order, so consecutive lanes store consecutive 8-B entries of one
+// bin's run instead of 64 scattered 8-B stores per wave instruction.  PPT points
+// per thread (S_THREADS * PPT entries staged, 8 B each).
+template <uint32_t PPT>
+static __global__ void __launch_bounds__(1024) k_msm_s1_scatter_st(const uint32_t* __restrict__ dig, uint32_t n,
+                                                                   uint32_t nb, uint32_t shared_stride, uint32_t F,
+                                                                   uint32_t NC, uint32_t nh,
+                                                                   uint32_t* __restrict__ ccursor,
+                                                                   uint64_t* __restrict__ tmp) {
+  constexpr uint32_t PTS = S_THREADS * PPT;
+  extern __shared__ uint64_t s1s_lds[];
+  uint64_t* stage = s1s_lds;
+  uint32_t* hist = reinterpret_cast<uint32_t*>(s1s_lds + PTS);
+  uint32_t* cur = hist + nh;   // global base of the block's run in bin q
+  uint32_t* lb = cur + nh;     // local base of bin q in the stage
+  uint32_t* wsum = lb + nh;    // 17 words
+  const uint32_t t = threadIdx.x, w = blockIdx.y, base = blockIdx.x * PTS;
+  const uint32_t wb = shared_stride ? 0u : w * nb;
+  const uint32_t h0 = nh == NC ? 0u : wb >> F;
+  for (uint32_t q = t; q < nh; q += S_THREADS) hist[q] = 0;
+  __syncthreads();
+  uint32_t dv[PPT], rk[PPT];
+#pragma unroll
+  for (uint32_t r = 0; r < PPT; r++) {
+    const uint32_t i = base + r * S_THREADS + t;
+    dv[r] = i < n ? dig[(size_t)w * n + i] : 0xffffffffu;
+    if (dv[r] != 0xffffffffu) rk[r] = lds_rank_add(hist, (((dv[r] & 0x7fffffffu) + wb) >> F) - h0);
+  }
+  __syncthreads();
+  for (uint32_t q = t; q < nh; q += S_THREADS) {
+    const uint32_t h = hist[q];
+    cur[q] = h ? atomicAdd(&ccursor[h0 + q], h) : 0u;
+    lb[q] = h;
+  }
+  const uint32_t total = block_excl_scan(lb, nh, wsum);  // synchronises
+#pragma unroll
+  for (uint32_t r = 0; r < PPT; r++) {
+    if (dv[r] == 0xffffffffu) continue;
+    const uint32_t i = base + r * S_THREADS + t;
+    const uint32_t b = (dv[r] & 0x7fffffffu) + wb;
+    const uint32_t v = (shared_stride ? w * shared_stride + i : i) | (dv[r] & 0x80000000u);
+    stage[lb[(b >> F) - h0] + rk[r]] = ((uint64_t)v << 32) | b;
+  }
+  __syncthreads();
+  for (uint32_t q = t; q < total; q += S_THREADS) {
+    const uint64_t e = stage[q];
+    const uint32_t h = ((uint32_t)e >> F) - h0;
+    tmp[cur[h] + (q - lb[h])] = e;
+  }
+}
+
 // block j -> (coarse bin, part): largest H with pbase[H] <= j
 // (no split bins, the usual case: part j is bin j)
 __device__ __forceinline__ void s2_locate(const uint32_t* __restrict__ pbase, uint32_t NC, uint32_t j, uint32_t* sh) {
@@ -379,8 +432,18 @@ int msm_sort_digits(gm_ctx* ctx, Arena& arena, const SortGeom& g, size_t n, uint
                      sbase.as<uint32_t>(), scursor.as<uint32_t>(), spbase.as<uint32_t>(), offsets);
   // bins one pass-1 block touches: its window's own nb >> shift in the plain layout
   const uint32_t nh = (!shared_stride && (1u << shift) <= nb) ? nb >> shift : g.NS;
-  hipLaunchKernelGGL(k_msm_s1_scatter, dim3(blocks_for(n, S1_PTS), W), dim3(S_THREADS), 2 * sizeof(uint32_t) * nh, st,
-                     dig, (uint32_t)n, nb, shared_stride, shift, g.NS, nh, scursor.as<uint32_t>(), tmp.as<uint64_t>());
+  // staged (coalesced-write) pass 1 while its LDS fits: 64 KB of entries plus
+  // three words per touched bin (GM_MSM_S1_STAGED=0: the direct scatter, A/B)
+  static const bool s1_staged = !getenv("GM_MSM_S1_STAGED") || atoi(getenv("GM_MSM_S1_STAGED")) != 0;
+  if (s1_staged && nh <= 4096) {
+    const size_t lds = 8 * (size_t)S1_PTS + sizeof(uint32_t) * (3 * (size_t)nh + 17);
+    hipLaunchKernelGGL(k_msm_s1_scatter_st<S1_PPT>, dim3(blocks_for(n, S1_PTS), W), dim3(S_THREADS), lds, st, dig,
+                       (uint32_t)n, nb, shared_stride, shift, g.NS, nh, scursor.as<uint32_t>(), tmp.as<uint64_t>());
+  } else {
+    hipLaunchKernelGGL(k_msm_s1_scatter, dim3(blocks_for(n, S1_PTS), W), dim3(S_THREADS), 2 * sizeof(uint32_t) * nh,
+                       st, dig, (uint32_t)n, nb, shared_stride, shift, g.NS, nh, scursor.as<uint32_t>(),
+                       tmp.as<uint64_t>());
+  }
   // final pass input: coarse-binned entries with their bases / part table
   const uint64_t* fin = tmp.as<uint64_t>();
   const uint32_t *cbase = sbase.as<uint32_t>(), *pbase = spbase.as<uint32_t>();
