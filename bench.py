@@ -390,7 +390,8 @@ def secondary(ctx, gm, args):
                 # proof (its check and the labelled CPU baseline of the headline workload)
                 res["groth16"].append(groth16_bench(ctx, gm, l, precompute=False,
                                                     check_oracle=("full" if l <= 20 else
-                                                                  "host" if not args.no_cpu_baseline else None)))
+                                                                  "host" if not args.no_cpu_baseline else None),
+                                                    staged=True))
             if not args.g16_no_precomputed:
                 res["groth16"].append(groth16_bench(ctx, gm, l, precompute=True))
     return res
@@ -468,7 +469,7 @@ def synthetic_pk(ctx, gm, n, nb_wires, nb_public, slices=None):
     return pk
 
 
-def groth16_bench(ctx, gm, logn, precompute=True, check_oracle=False):
+def groth16_bench(ctx, gm, logn, precompute=True, check_oracle=False, staged=False):
     """Groth16 prove at n = 2^logn (synthetic pk of random points, synthetic
     solution vectors), timed in two scopes:
       host:   wires / a / b / c in host memory, gm_g16_prove -- the scope of
@@ -478,7 +479,8 @@ def groth16_bench(ctx, gm, logn, precompute=True, check_oracle=False):
     compared with the oracle prover (prove.go:62-325 restatement) on the same key
     and inputs, plus the staged scopes and the key I/O; "host" -- the staged
     scopes and the host-scope proof only (one oracle prove: the 2^24 headline's
-    check and CPU baseline)."""
+    check and CPU baseline).  staged: the staged scopes also without an oracle
+    check (their proofs are compared with the host-scope proof)."""
     import numpy as np
     n = 1 << logn
     nb_wires = n + 2
@@ -554,7 +556,7 @@ def groth16_bench(ctx, gm, logn, precompute=True, check_oracle=False):
                     "gm_g16_prove_r1cs); r1cs_resident_wires_staged = the same with the wires staged during "
                     "Solve (gm_g16_stage_prove_r1cs, the Go default path with the wire level hook); all after "
                     "Solve"}
-    if check_oracle:
+    if check_oracle or staged:
         res.update(staged_bench(ctx, dpk, n, host, r, proof))
     if check_oracle == "full":
         res.update(io_bench(ctx, gm, dpk, pk, n, nb_wires, nb_public, host, r, proof))

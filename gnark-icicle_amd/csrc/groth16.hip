@@ -538,22 +538,6 @@ struct HostStagedH : HSource {
   HostStagedH(gm_ctx* x, gm_g16_pk* k, void* a_, void* b_, void* c_, const void* ha_, const void* hb_,
               const void* hc_, size_t n_)
       : ctx(x), pk(k), da(a_), db(b_), dc(c_), ha(ha_), hb(hb_), hc(hc_), nc(n_) {}
-  // memcpy split over `nt` threads (the ring's host-side fill: one thread copies
-  // pageable memory at ~21 GB/s, slower than the DMA behind it)
-  static void par_memcpy(void* dst, const void* src, size_t len, int nt) {
-    if (nt <= 1 || len < (size_t(4) << 20)) {
-      memcpy(dst, src, len);
-      return;
-    }
-    const size_t part = (len / nt + 4095) & ~size_t(4095);
-    std::vector<std::thread> ws;
-    for (int i = 1; i < nt && (size_t)i * part < len; i++) {
-      const size_t o = (size_t)i * part;
-      ws.emplace_back([=] { memcpy((char*)dst + o, (const char*)src + o, std::min(part, len - o)); });
-    }
-    memcpy(dst, src, std::min(part, len));
-    for (auto& w : ws) w.join();
-  }
   int start() {
     int rc;
     if ((rc = ev.create())) return rc;
@@ -568,8 +552,6 @@ struct HostStagedH : HSource {
     // the DMA's 0.59 ms and a, b, c arrived only ~75 ms into a 2^24 prove
     // (profiles/r05i_host_prove_timeline.txt).
     static const bool pinned = !getenv("GM_G16_H2D_PINNED") || atoi(getenv("GM_G16_H2D_PINNED")) != 0;
-    static const int fill_threads =
-        getenv("GM_G16_H2D_THREADS") ? std::max(1, std::min(16, atoi(getenv("GM_G16_H2D_THREADS")))) : 4;
     th = std::thread([this] {
       int r = GM_OK;
       if (hipSetDevice(ctx->device) != hipSuccess) r = GM_ERR_DEVICE;
@@ -597,7 +579,7 @@ struct HostStagedH : HSource {
             const size_t len = std::min(gm_ctx::H2D_SLOT, 32 * nc - off);
             if (used[slot] && hipEventSynchronize(ctx->h2d_ev[slot]) != hipSuccess) r = GM_ERR_DEVICE;
             if (r) break;
-            par_memcpy(ctx->h2d_pin[slot], (const char*)src[k] + off, len, fill_threads);
+            par_memcpy(ctx->h2d_pin[slot], (const char*)src[k] + off, len, h2d_fill_threads());
             if (hipMemcpyAsync((char*)dst[k] + off, ctx->h2d_pin[slot], len, hipMemcpyHostToDevice, ctx->copy) !=
                     hipSuccess ||
                 hipEventRecord(ctx->h2d_ev[slot], ctx->copy) != hipSuccess)

@@ -552,7 +552,7 @@ int gm_g16_stage_put_range(gm_g16_stage* st, int which, size_t lo, size_t count,
     const size_t cnt = std::min(per, count - o);
     int k;
     if (int rc = st->take(&k)) return rc;
-    memcpy(st->host[k], (const char*)host_src + 32 * o, 32 * cnt);
+    par_memcpy(st->host[k], (const char*)host_src + 32 * o, 32 * cnt, h2d_fill_threads());
     GM_HIP(hipMemcpyAsync((char*)st->vec[which] + 32 * (lo + o), st->host[k], 32 * cnt, hipMemcpyHostToDevice,
                           ctx->copy));
     GM_HIP(hipEventRecord(st->ev[k], ctx->copy));

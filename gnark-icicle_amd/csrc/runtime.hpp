@@ -3,10 +3,14 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/gnark_mi355x.h"
@@ -201,6 +205,31 @@ struct Arena {
     return GM_OK;
   }
 };
+
+// Host-side fill of a pinned staging slot: memcpy split over `nt` threads.  One
+// thread copies pageable memory at ~21 GB/s, below the ~57 GB/s DMA behind it
+// (a 32 MiB slot: 1.55 ms of memcpy against 0.59 ms of copy,
+// profiles/r05i_host_prove_timeline.txt).
+inline void par_memcpy(void* dst, const void* src, size_t len, int nt) {
+  if (nt <= 1 || len < (size_t(4) << 20)) {
+    memcpy(dst, src, len);
+    return;
+  }
+  const size_t part = (len / nt + 4095) & ~size_t(4095);
+  std::vector<std::thread> ws;
+  for (int i = 1; i < nt && (size_t)i * part < len; i++) {
+    const size_t o = (size_t)i * part;
+    ws.emplace_back([=] { memcpy((char*)dst + o, (const char*)src + o, std::min(part, len - o)); });
+  }
+  memcpy(dst, src, std::min(part, len));
+  for (auto& w : ws) w.join();
+}
+// threads per pinned-slot fill: GM_G16_H2D_THREADS (1..16), default 4
+inline int h2d_fill_threads() {
+  static const int n =
+      getenv("GM_G16_H2D_THREADS") ? std::max(1, std::min(16, atoi(getenv("GM_G16_H2D_THREADS")))) : 4;
+  return n;
+}
 
 // A deferred-tail arena slot of the context (at most MSM_SLOTS MSMs in flight).
 // ctx->stream temporarily replaced (all MSM code queues on ctx->stream)
