@@ -173,6 +173,8 @@ int gm_destroy(gm_ctx* ctx) {
     if (s) hipStreamSynchronize(s);
   if (ctx->g16_stream) hipStreamSynchronize(ctx->g16_stream);
   orphan_pending_msms(ctx);
+  for (auto& pr : ctx->pending_reads) hipEventDestroy(pr.second);
+  ctx->pending_reads.clear();
   ntt_domains_free(ctx);
   for (gm::ArenaState* a : {&ctx->arena, &ctx->slots[0], &ctx->slots[1], &ctx->slots[2]}) {
     for (auto& ch : a->chunks) hipFree(ch.base);
@@ -203,7 +205,7 @@ int gm_destroy(gm_ctx* ctx) {
 
 int gm_trim(gm_ctx* ctx) {
   if (!ctx) return GM_ERR_INVALID;
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   if (!ctx->live_msms.empty()) {
     set_error("gm_trim: MSMs are pending on this context (gm_msm_wait them first)");
     return GM_ERR_INVALID;
@@ -232,7 +234,7 @@ int gm_trim(gm_ctx* ctx) {
 }
 
 int gm_synchronize(gm_ctx* ctx) {
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   GM_HIP(hipStreamSynchronize(ctx->stream));
   prof_collect(ctx);
@@ -240,19 +242,19 @@ int gm_synchronize(gm_ctx* ctx) {
 }
 
 int gm_profile_enable(gm_ctx* ctx, int on) {
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   ctx->profiling = on != 0;
   return GM_OK;
 }
 int gm_profile_reset(gm_ctx* ctx) {
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   hipStreamSynchronize(ctx->stream);
   prof_collect(ctx);
   ctx->stats.clear();
   return GM_OK;
 }
 int gm_profile_get(gm_ctx* ctx, const char* name, double* total_ms, uint64_t* count) {
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   hipStreamSynchronize(ctx->stream);
   prof_collect(ctx);
   auto it = ctx->stats.find(name);
@@ -266,7 +268,7 @@ int gm_profile_get(gm_ctx* ctx, const char* name, double* total_ms, uint64_t* co
   return GM_OK;
 }
 int gm_profile_dump(gm_ctx* ctx, char* buf, size_t cap) {
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   hipStreamSynchronize(ctx->stream);
   prof_collect(ctx);
   std::string s;
@@ -287,14 +289,14 @@ int gm_set_msm_window(gm_ctx* ctx, int c) {
 
 int gm_set_msm_glv(gm_ctx* ctx, int mode) {
   if (!ctx || mode < -1 || mode > 1) return GM_ERR_INVALID;
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   ctx->msm_glv = mode;
   return GM_OK;
 }
 
 // ---- memory -----------------------------------------------------------------
 int gm_malloc(gm_ctx* ctx, size_t bytes, void** dev_out) {
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   hipError_t e = hipMalloc(dev_out, bytes ? bytes : 16);
   if (e != hipSuccess) {
@@ -304,28 +306,28 @@ int gm_malloc(gm_ctx* ctx, size_t bytes, void** dev_out) {
   return GM_OK;
 }
 int gm_free(gm_ctx* ctx, void* dev) {
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   GM_HIP(hipStreamSynchronize(ctx->stream));
   GM_HIP(hipFree(dev));
   return GM_OK;
 }
 int gm_memcpy_h2d(gm_ctx* ctx, void* dev, const void* host, size_t bytes) {
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   GM_HIP(hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, ctx->stream));
   GM_HIP(hipStreamSynchronize(ctx->stream));
   return GM_OK;
 }
 int gm_memcpy_d2h(gm_ctx* ctx, void* host, const void* dev, size_t bytes) {
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   GM_HIP(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, ctx->stream));
   GM_HIP(hipStreamSynchronize(ctx->stream));
   return GM_OK;
 }
 int gm_memcpy_d2d(gm_ctx* ctx, void* dst, const void* src, size_t bytes) {
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   GM_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, ctx->stream));
   GM_HIP(hipStreamSynchronize(ctx->stream));
@@ -347,7 +349,7 @@ int gm_msm(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const void* 
            size_t n, void* out_jac, void* out_affine) {
   if (!ctx) return GM_ERR_INVALID;
   if (int rc = check_curve(curve)) return rc;
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   int rc;
   if (curve == GM_BN254)
@@ -425,6 +427,7 @@ int gm_msm_async(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const 
                  gm_msm_pending** out) {
   if (!ctx || !out) return GM_ERR_INVALID;
   if (int rc = check_curve(curve)) return rc;
+  // no CtxLock: nothing is queued on ctx->stream here (gm_ctx::pending_reads)
   std::lock_guard<std::recursive_mutex> g(ctx->mu);
   GM_HIP(hipSetDevice(ctx->device));
   auto* p = new gm_msm_pending(ctx);
@@ -438,17 +441,39 @@ int gm_msm_async(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const 
   // (profiles/r04m_hwq_ab.txt).  It starts after the work already queued on
   // ctx->stream (the inputs).
   static const bool slot_streams = !getenv("GM_MSM_SLOT_STREAMS") || atoi(getenv("GM_MSM_SLOT_STREAMS")) != 0;
-  const hipStream_t main_st = ctx->stream;
   hipEvent_t inputs_read = nullptr;
   p->st = ctx->stream;
   if (rc == GM_OK && slot_streams) {
     hipStream_t& ss = ctx->slot_stream[p->slot.k];
-    if (!ss) GM_HIP(hipStreamCreateWithFlags(&ss, hipStreamNonBlocking));
-    hipEvent_t ev;
-    GM_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    GM_HIP(hipEventRecord(ev, ctx->stream));
-    GM_HIP(hipStreamWaitEvent(ss, ev, 0));
-    GM_HIP(hipEventDestroy(ev));
+    // The slot streams run at the highest stream priority: the runtime keeps a
+    // separate pool of hardware queues per priority, so with the default four
+    // queues they do not share one with ctx->stream / aux / copy or each other,
+    // and the next MSM's conversion and sort start beside this one's reduction
+    // (bench 2^20: 599-605 -> 632-645 Mpoints/s with the change below,
+    // profiles/r05r_slot_stream_ab.txt).  GM_MSM_SLOT_PRIO=0: normal priority.
+    static const bool prio = !getenv("GM_MSM_SLOT_PRIO") || atoi(getenv("GM_MSM_SLOT_PRIO")) != 0;
+    if (!ss) {
+      if (prio) {
+        int least = 0, greatest = 0;
+        GM_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        GM_HIP(hipStreamCreateWithPriority(&ss, hipStreamNonBlocking, greatest));
+      } else {
+        GM_HIP(hipStreamCreateWithFlags(&ss, hipStreamNonBlocking));
+      }
+    }
+    // Ordered after the work already queued on ctx->stream (the inputs) -- by a
+    // marker only when that stream still has work: a packet on ctx->stream waits
+    // behind everything in its hardware queue, which may be shared with a slot
+    // stream running the previous MSM.
+    const hipError_t q = hipStreamQuery(ctx->stream);
+    (void)hipGetLastError();  // hipErrorNotReady is an answer, not an error
+    if (q != hipSuccess) {
+      hipEvent_t ev;
+      GM_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+      GM_HIP(hipEventRecord(ev, ctx->stream));
+      GM_HIP(hipStreamWaitEvent(ss, ev, 0));
+      GM_HIP(hipEventDestroy(ev));
+    }
     p->st = ss;
     // work queued later on ctx->stream (synchronous calls that may overwrite the
     // scalars or points in place) waits until this MSM has read them: the event is
@@ -469,18 +494,13 @@ int gm_msm_async(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const 
                 : msm_device_launch<CurveBLS12377, false>(ctx, a, sc, pt, n, false, nullptr, p->tail, inputs_read);
     }
   }
-  if (inputs_read) {
-    hipError_t e = rc == GM_OK ? hipStreamWaitEvent(main_st, inputs_read, 0) : hipSuccess;
-    hipEventDestroy(inputs_read);
-    if (e != hipSuccess) {
-      set_error(std::string("gm_msm_async: hipStreamWaitEvent: ") + hipGetErrorString(e));
-      rc = GM_ERR_DEVICE;
-    }
-  }
+  if (inputs_read && rc) hipEventDestroy(inputs_read);
   if (rc) {
     delete p;
     return rc;
   }
+  // ctx->stream waits on it at the next call that may queue work there (CtxLock)
+  if (inputs_read) ctx->pending_reads.push_back({p, inputs_read});
   ctx->live_msms.push_back(p);
   *out = p;
   return GM_OK;
@@ -494,9 +514,18 @@ int gm_msm_wait(gm_msm_pending* p, void* out_jac, void* out_affine) {
     set_error("gm_msm_wait: the context was destroyed while this MSM was pending");
     return GM_ERR_INVALID;
   }
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  std::lock_guard<std::recursive_mutex> g(ctx->mu);  // nothing queued on ctx->stream
   auto& live = ctx->live_msms;
   live.erase(std::remove(live.begin(), live.end(), p), live.end());
+  // a finished MSM has read its inputs: ctx->stream need not wait for it
+  auto& pr = ctx->pending_reads;
+  for (auto it = pr.begin(); it != pr.end();)
+    if (it->first == p) {
+      hipEventDestroy(it->second);
+      it = pr.erase(it);
+    } else {
+      ++it;
+    }
   GM_HIP(hipSetDevice(ctx->device));
   int rc;
   StreamSwap sw(ctx, p->st);  // a long-span redo runs on the MSM's own stream
@@ -513,7 +542,7 @@ int gm_msm_wait(gm_msm_pending* p, void* out_jac, void* out_affine) {
 int gm_msm_host_scalars(gm_ctx* ctx, int curve, int g2, const void* scalars_host,
                         const void* points_dev, size_t n, void* out_jac, void* out_affine) {
   if (!ctx || (n && !scalars_host)) return GM_ERR_INVALID;
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   Arena arena(ctx);
   DevBuf s;
@@ -526,7 +555,7 @@ int gm_msm_host_scalars(gm_ctx* ctx, int curve, int g2, const void* scalars_host
 int gm_points_upload(gm_ctx* ctx, int curve, int g2, const void* host_points, size_t n, void** out) {
   if (!ctx || !out) return GM_ERR_INVALID;
   if (int rc = check_curve(curve)) return rc;
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   const size_t gb = fp_bytes(curve) * (g2 ? 4 : 2) * n;
   const size_t ib = n * (curve == GM_BN254 ? (g2 ? msm_internal_point_bytes<CurveBN254, true>()
@@ -575,7 +604,7 @@ int gm_msm_prepared(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, con
                     void* out_jac, void* out_affine) {
   if (!ctx) return GM_ERR_INVALID;
   if (int rc = check_curve(curve)) return rc;
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   int rc;
   if (curve == GM_BN254)
@@ -625,7 +654,7 @@ int gm_points_upload_precomputed(gm_ctx* ctx, int curve, int g2, const void* hos
     set_error("precompute: copies * n must be < 2^31");
     return GM_ERR_INVALID;
   }
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   const size_t gb = fp_bytes(curve) * (g2 ? 4 : 2) * n;
   const size_t ib = (size_t)pre.W * n *
@@ -664,7 +693,7 @@ int gm_msm_precomputed(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, 
   }
   MsmPrecomp pre;
   if (int rc = make_precomp(curve, prepared_n, window, &pre)) return rc;
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   int rc;
   if (curve == GM_BN254)
@@ -684,7 +713,7 @@ int gm_kzg_commit(gm_ctx* ctx, int curve, const void* srs, size_t srs_len, const
     set_error("kzg commit: polynomial larger than the SRS");
     return GM_ERR_INVALID;
   }
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   Arena arena(ctx);
   DevBuf s;
@@ -697,7 +726,7 @@ int gm_kzg_commit(gm_ctx* ctx, int curve, const void* srs, size_t srs_len, const
 // ---- NTT --------------------------------------------------------------------------
 int gm_ntt(gm_ctx* ctx, int curve, void* data_dev, size_t n, int inverse, int dit, int coset) {
   if (int rc = check_curve(curve)) return rc;
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   int rc = curve == GM_BN254 ? ntt_device<CurveBN254>(ctx, data_dev, n, inverse, dit, coset)
                              : ntt_device<CurveBLS12377>(ctx, data_dev, n, inverse, dit, coset);
@@ -709,7 +738,7 @@ int gm_ntt(gm_ctx* ctx, int curve, void* data_dev, size_t n, int inverse, int di
 int gm_poly_ops(gm_ctx* ctx, int curve, void* a, const void* b, const void* c, size_t n,
                 const void* den_host) {
   if (int rc = check_curve(curve)) return rc;
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   int rc = curve == GM_BN254 ? poly_ops_device<CurveBN254>(ctx, a, b, c, n, den_host)
                              : poly_ops_device<CurveBLS12377>(ctx, a, b, c, n, den_host);
@@ -720,7 +749,7 @@ int gm_poly_ops(gm_ctx* ctx, int curve, void* a, const void* b, const void* c, s
 }
 int gm_reverse_scalars(gm_ctx* ctx, int curve, void* data_dev, size_t n) {
   if (int rc = check_curve(curve)) return rc;
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   int rc = curve == GM_BN254 ? reverse_device<CurveBN254>(ctx, data_dev, n)
                              : reverse_device<CurveBLS12377>(ctx, data_dev, n);
@@ -731,7 +760,7 @@ int gm_reverse_scalars(gm_ctx* ctx, int curve, void* data_dev, size_t n) {
 }
 int gm_groth16_compute_h(gm_ctx* ctx, int curve, void* a, void* b, void* c, size_t len, size_t n) {
   if (int rc = check_curve(curve)) return rc;
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   int rc = curve == GM_BN254 ? compute_h_device<CurveBN254>(ctx, a, b, c, len, n)
                              : compute_h_device<CurveBLS12377>(ctx, a, b, c, len, n);
@@ -792,7 +821,7 @@ int gm_generator(int curve, int g2, void* out) {
 
 int gm_random_scalars(gm_ctx* ctx, int curve, uint64_t seed, size_t n, void* scalars_dev) {
   if (int rc = check_curve(curve)) return rc;
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   if (curve == GM_BN254)
     hipLaunchKernelGGL(k_random_scalars<Bn254Fr>, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream,
@@ -822,7 +851,7 @@ static int batch_mul_t(gm_ctx* ctx, const void* base, const void* sc, size_t n, 
 int gm_batch_mul_base(gm_ctx* ctx, int curve, int g2, const void* base, const void* sc, size_t n,
                       void* out) {
   if (int rc = check_curve(curve)) return rc;
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   if (curve == GM_BN254)
     return g2 ? batch_mul_t<CurveBN254, true>(ctx, base, sc, n, out)

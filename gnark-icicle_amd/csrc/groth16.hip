@@ -1178,7 +1178,7 @@ int gm_g16_pk_upload_shard(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsi
     set_error("pk upload: bad rank / world");
     return GM_ERR_INVALID;
   }
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   Ranges rg;
   shard_of(h->nbA, rank, world, &rg.loA, &rg.hiA);
@@ -1197,7 +1197,7 @@ int gm_g16_pk_precomputed(const gm_g16_pk* pk, int* out) {
 
 int gm_g16_pk_free(gm_ctx* ctx, gm_g16_pk* pk) {
   if (!pk) return GM_OK;
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   hipSetDevice(ctx->device);
   pk_release(pk);
   return GM_OK;
@@ -1210,7 +1210,7 @@ int gm_g16_prove_device(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, void*
     set_error("prove: more constraints than the domain size");
     return GM_ERR_INVALID;
   }
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   int rc = pk->curve == GM_BN254 ? g16_prove_t<CurveBN254>(ctx, pk, wires_dev, a, b, c, nullptr, nullptr, nullptr,
                                                            nc, r, s, ar_out, bs_out, krs_out)
@@ -1230,7 +1230,7 @@ int gm_g16_prove(gm_ctx* ctx, gm_g16_pk* pk, const void* wires, const void* a, c
     set_error("prove: more constraints than the domain size");
     return GM_ERR_INVALID;
   }
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   Arena arena(ctx);
   DevBuf w;
@@ -1273,7 +1273,7 @@ int gm_g16_prove(gm_ctx* ctx, gm_g16_pk* pk, const void* wires, const void* a, c
 int gm::g16_prove_r1cs_device(gm_ctx* ctx, gm_g16_pk* pk, const gm_r1cs* r1, const void* wires_dev, void* a,
                               void* b, void* c, const void* r, const void* s, void* ar_out, void* bs_out,
                               void* krs_out) {
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   const size_t nc = r1cs_nb_constraints(r1);
   int rc = pk->curve == GM_BN254
@@ -1300,7 +1300,7 @@ int gm_g16_prove_r1cs(gm_ctx* ctx, gm_g16_pk* pk, const gm_r1cs* r1, const void*
               "whole key)");
     return GM_ERR_INVALID;
   }
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   Arena arena(ctx);
   DevBuf w, da, db, dc;
@@ -1326,7 +1326,7 @@ int gm_g16_prove_partial(gm_ctx* ctx, gm_g16_pk* pk, const void* wires_dev, void
     set_error("prove: more constraints than the domain size");
     return GM_ERR_INVALID;
   }
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   auto run = [&](auto tag) -> int {
     using C = decltype(tag);
@@ -1452,7 +1452,7 @@ int gm_g16_pk_upload_multi(gm_multi* m, int curve, const gm_g16_pk_host* h, unsi
   for (int d = 0; d < nd; d++) {
     th.emplace_back([&, d] {
       gm_ctx* ctx = m->ctx[d];
-      std::lock_guard<std::recursive_mutex> g(ctx->mu);
+      gm::CtxLock g(ctx);
       if (hipSetDevice(ctx->device) != hipSuccess) {
         rcs[d] = GM_ERR_DEVICE;
         errs[d] = "hipSetDevice failed";
@@ -1577,7 +1577,7 @@ int g16_prove_multi_t(gm_multi* m, gm_g16_pk_multi* mp, const uint8_t* wires, co
         }
       }
     };
-    std::lock_guard<std::recursive_mutex> g(ctx->mu);
+    gm::CtxLock g(ctx);
     if (hipSetDevice(ctx->device) != hipSuccess) {
       if (d == chain_dev[0]) chain_done[0].signal(GM_ERR_DEVICE);
       if (d == chain_dev[1]) chain_done[1].signal(GM_ERR_DEVICE);

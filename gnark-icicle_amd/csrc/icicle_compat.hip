@@ -58,7 +58,7 @@ int gm_icicle_generate_twiddles(gm_ctx* ctx, int curve, size_t n, int inverse, v
   (void)inverse;  // one cached domain serves both directions
   if (!ctx || !token_out) return GM_ERR_INVALID;
   if (int rc = check_curve_id(curve)) return rc;
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   int rc = curve == GM_BN254 ? ntt_domain_prepare<CurveBN254>(ctx, n) : ntt_domain_prepare<CurveBLS12377>(ctx, n);
   if (rc) return rc;
@@ -75,7 +75,7 @@ int gm_icicle_generate_twiddles(gm_ctx* ctx, int curve, size_t n, int inverse, v
 int gm_icicle_intt_on_device(gm_ctx* ctx, int curve, void* in_dev, size_t n, int coset, void** out_dev) {
   if (!ctx || !in_dev || !out_dev) return GM_ERR_INVALID;
   if (int rc = check_curve_id(curve)) return rc;
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   void* out = nullptr;
   hipError_t e = hipMalloc(&out, 32 * (n ? n : 1));
@@ -101,7 +101,7 @@ int gm_icicle_intt_on_device(gm_ctx* ctx, int curve, void* in_dev, size_t n, int
 int gm_icicle_ntt_on_device(gm_ctx* ctx, int curve, void* out_dev, const void* in_dev, size_t n, int coset) {
   if (!ctx || !in_dev || !out_dev) return GM_ERR_INVALID;
   if (int rc = check_curve_id(curve)) return rc;
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   int rc = curve == GM_BN254 ? ntt_into<CurveBN254>(ctx, out_dev, in_dev, n, coset != 0)
                              : ntt_into<CurveBLS12377>(ctx, out_dev, in_dev, n, coset != 0);
@@ -115,7 +115,7 @@ int gm_icicle_poly_ops(gm_ctx* ctx, int curve, void* a_dev, const void* b_dev, c
                        const void* den_dev, size_t n) {
   if (!ctx || !a_dev || !b_dev || !c_dev || !den_dev) return GM_ERR_INVALID;
   if (int rc = check_curve_id(curve)) return rc;
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   int rc = curve == GM_BN254 ? poly_ops_vec_device<CurveBN254>(ctx, a_dev, b_dev, c_dev, den_dev, n)
                              : poly_ops_vec_device<CurveBLS12377>(ctx, a_dev, b_dev, c_dev, den_dev, n);

@@ -282,7 +282,7 @@ int gm_g16_pk_upload_dump_shard(gm_ctx* ctx, int curve, const gm_g16_pk_host* me
     set_error("pk dump: bad rank / world");
     return GM_ERR_INVALID;
   }
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   // slice table: (count, first point byte) of each of the five WriteSlice records
   const size_t expect[5] = {meta->nbA, meta->nbB, meta->domain_size - 1, meta->nbK, meta->nbB};
@@ -329,7 +329,7 @@ int gm_g16_pk_upload_dump(gm_ctx* ctx, int curve, const gm_g16_pk_host* meta, in
 
 int gm_g16_pk_save_cache(gm_ctx* ctx, const gm_g16_pk* pk, int fd) {
   if (!ctx || !pk || fd < 0) return GM_ERR_INVALID;
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   CacheHeader h;
   memset(&h, 0, sizeof(h));
@@ -377,7 +377,7 @@ int gm_g16_pk_save_cache(gm_ctx* ctx, const gm_g16_pk* pk, int fd) {
 
 int gm_g16_pk_load_cache(gm_ctx* ctx, int fd, gm_g16_pk** out) {
   if (!ctx || !out || fd < 0) return GM_ERR_INVALID;
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   CacheHeader h;
   int rc;
@@ -500,7 +500,7 @@ int gm_g16_stage_begin(gm_ctx* ctx, gm_g16_pk* pk, size_t nb_constraints, gm_g16
     set_error("stage: more constraints than the domain size");
     return GM_ERR_INVALID;
   }
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   if (gm_g16_stage* sp = pk->spare_stage; sp && sp->ctx == ctx) {
     // the key's buffers of a previous proof (gm_g16_stage_free parked them)
@@ -545,7 +545,7 @@ int gm_g16_stage_put_range(gm_g16_stage* st, int which, size_t lo, size_t count,
     return GM_ERR_INVALID;
   }
   gm_ctx* ctx = st->ctx;
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   const size_t per = gm_g16_stage::SLOT / 32;
   for (size_t o = 0; o < count; o += per) {
@@ -563,7 +563,7 @@ int gm_g16_stage_put_range(gm_g16_stage* st, int which, size_t lo, size_t count,
 int gm_g16_stage_put_indexed(gm_g16_stage* st, int which, const void* host_base, const uint32_t* idx, size_t k) {
   if (!st || which < 0 || which > 3 || (k && (!host_base || !idx))) return GM_ERR_INVALID;
   gm_ctx* ctx = st->ctx;
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   // a slot holds per records: per u32 indices, then per 32-B values (16-B aligned)
   const size_t per = (gm_g16_stage::SLOT - 16) / 36 & ~size_t(3);
@@ -599,7 +599,7 @@ int gm_g16_stage_prove(gm_g16_stage* st, const void* r, const void* s, void* ar_
   if (!st) return GM_ERR_INVALID;
   gm_ctx* ctx = st->ctx;
   {
-    std::lock_guard<std::recursive_mutex> g(ctx->mu);
+    gm::CtxLock g(ctx);
     GM_HIP(hipSetDevice(ctx->device));
     GM_HIP(hipStreamSynchronize(ctx->copy));
   }
@@ -617,7 +617,7 @@ int gm_g16_stage_prove_r1cs(gm_g16_stage* st, const gm_r1cs* r1, const void* r, 
     return GM_ERR_INVALID;
   }
   {
-    std::lock_guard<std::recursive_mutex> g(ctx->mu);
+    gm::CtxLock g(ctx);
     GM_HIP(hipSetDevice(ctx->device));
     GM_HIP(hipStreamSynchronize(ctx->copy));
   }
@@ -628,7 +628,7 @@ int gm_g16_stage_prove_r1cs(gm_g16_stage* st, const gm_r1cs* r1, const void* r, 
 
 int gm_g16_stage_free(gm_g16_stage* st) {
   if (!st) return GM_OK;
-  std::lock_guard<std::recursive_mutex> g(st->ctx->mu);
+  gm::CtxLock g(st->ctx);
   hipSetDevice(st->ctx->device);
   hipStreamSynchronize(st->ctx->copy);
   // Park the buffers with the key for its next proof (one spare per key): a

@@ -146,7 +146,7 @@ int gm_r1cs_upload(gm_ctx* ctx, int curve, size_t nb_constraints, size_t nb_wire
       }
     }
   }
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   auto* r = new gm_r1cs();
   r->curve = curve;
@@ -191,7 +191,7 @@ int gm_r1cs_upload(gm_ctx* ctx, int curve, size_t nb_constraints, size_t nb_wire
 int gm_r1cs_free(gm_ctx* ctx, gm_r1cs* r) {
   if (!r) return GM_OK;
   if (ctx) {
-    std::lock_guard<std::recursive_mutex> g(ctx->mu);
+    gm::CtxLock g(ctx);
     hipSetDevice(ctx->device);
     hipStreamSynchronize(ctx->stream);
   }
@@ -201,7 +201,7 @@ int gm_r1cs_free(gm_ctx* ctx, gm_r1cs* r) {
 
 int gm_r1cs_eval(gm_ctx* ctx, const gm_r1cs* r, const void* wires_dev, void* a_dev, void* b_dev, void* c_dev) {
   if (!ctx || !r || (r->nc && (!wires_dev || !a_dev || !b_dev || !c_dev))) return GM_ERR_INVALID;
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   int rc = r1cs_eval_device(ctx, r, wires_dev, a_dev, b_dev, c_dev);
   if (rc) return rc;

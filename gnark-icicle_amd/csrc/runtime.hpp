@@ -11,6 +11,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <utility>
 #include <vector>
 
 #include "../../include/gnark_mi355x.h"
@@ -93,6 +94,14 @@ struct gm_ctx {
   // releases their slot / readback buffer and orphans them (gm_msm_wait then
   // fails with GM_ERR_INVALID and frees the handle)
   std::vector<gm_msm_pending*> live_msms;
+  // "inputs read" events of pending gm_msm_async MSMs (recorded on their slot
+  // streams after the digits and the point conversion).  Work queued later on
+  // ctx->stream must not overwrite those inputs first: every API call that may
+  // queue on ctx->stream takes the context through CtxLock, which makes
+  // ctx->stream wait on these events first.  gm_msm_async / gm_msm_wait put
+  // nothing on ctx->stream, so back-to-back async MSMs never meet a packet of
+  // it in a hardware queue they share.
+  std::vector<std::pair<const void*, hipEvent_t>> pending_reads;
   // a / b / c of a host-input prove (gm_g16_prove): their own allocation, outside
   // the workspace arena.  The runtime orders a pageable copy into an allocation
   // after the queued commands that use the same allocation, so copies into an
@@ -204,6 +213,23 @@ struct Arena {
     *out = p;
     return GM_OK;
   }
+};
+
+// ctx->stream waits until every pending async MSM has read its inputs (see
+// gm_ctx::pending_reads); a failed wait falls back to a host wait.
+inline void flush_pending_reads(gm_ctx* c) {
+  if (c->pending_reads.empty()) return;
+  hipSetDevice(c->device);
+  for (auto& pr : c->pending_reads) {
+    if (hipStreamWaitEvent(c->stream, pr.second, 0) != hipSuccess) hipEventSynchronize(pr.second);
+    hipEventDestroy(pr.second);
+  }
+  c->pending_reads.clear();
+}
+// The context's lock for API calls that may queue work on ctx->stream.
+struct CtxLock {
+  std::lock_guard<std::recursive_mutex> g;
+  explicit CtxLock(gm_ctx* c) : g(c->mu) { flush_pending_reads(c); }
 };
 
 // Host-side fill of a pinned staging slot: memcpy split over `nt` threads.  One

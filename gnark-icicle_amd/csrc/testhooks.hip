@@ -104,7 +104,7 @@ static int point_op_t(gm_ctx* ctx, int op, const void* a, const void* b, void* o
 extern "C" {
 int gm_test_field_op(gm_ctx* ctx, int curve, int kind, int op, const void* a_dev, const void* b_dev,
                      void* out_dev, size_t n) {
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   if (kind < 0 || kind > 2) return GM_ERR_INVALID;
   return curve == GM_BN254 ? field_op_t<CurveBN254>(ctx, kind, op, a_dev, b_dev, out_dev, n)
@@ -112,7 +112,7 @@ int gm_test_field_op(gm_ctx* ctx, int curve, int kind, int op, const void* a_dev
 }
 int gm_test_point_op(gm_ctx* ctx, int curve, int g2, int op, const void* a_dev, const void* b_dev,
                      void* out_dev, size_t n) {
-  std::lock_guard<std::recursive_mutex> g(ctx->mu);
+  gm::CtxLock g(ctx);
   GM_HIP(hipSetDevice(ctx->device));
   if (curve == GM_BN254)
     return g2 ? point_op_t<CurveBN254, true>(ctx, op, a_dev, b_dev, out_dev, n)

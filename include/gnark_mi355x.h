@@ -102,11 +102,15 @@ int gm_msm(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const void* 
  * and the Horner combination) and frees the handle.  The host tail of one MSM
  * thus overlaps the device work of the next one issued before it.  At most three
  * MSMs may be in flight per context; wait in issue order.  Each in-flight MSM
- * runs on a stream of its own (GM_MSM_SLOT_STREAMS=0: the context stream), so
- * one MSM's reduction overlaps the next one's accumulation when the process has
- * a hardware queue per stream (GPU_MAX_HW_QUEUES=8 before HIP initialises;
- * HIP's default 4 serialises them; the library raises the process default to 8
- * at load time when the variable is unset).  Synchronous calls
+ * runs on a stream of its own (GM_MSM_SLOT_STREAMS=0: the context stream), at
+ * the highest stream priority (a hardware-queue pool of their own, so they do
+ * not share a queue with the context's other streams; GM_MSM_SLOT_PRIO=0: normal
+ * priority), so one MSM's reduction overlaps the next one's conversion and sort.
+ * The MSM starts after the work already queued on the context stream (its
+ * inputs).  gm_msm_async and gm_msm_wait queue nothing on the context stream;
+ * the next call that does waits there for the pending MSMs' input reads first.
+ * (The library also raises GPU_MAX_HW_QUEUES to 8 at load time when the
+ * variable is unset.)  Synchronous calls
  * (gm_msm, gm_msm_prepared, gm_ntt, ...) may be made on the same context while
  * async MSMs are pending: each pending MSM keeps its own scratch arena and its
  * own pinned readback buffer until its gm_msm_wait, and work queued on the

@@ -463,6 +463,37 @@ def test_msm_async_interleaved_with_sync(gm_ctx, oracle):
             d[3].free()
 
 
+def test_msm_async_after_queued_producer(gm_ctx, oracle):
+    """gm_msm_async orders its MSM after the work already queued on the context
+    stream (a marker only when that stream is busy, csrc/capi.hip): the scalars
+    are produced by an in-place NTT and the points by a d2d copy queued right
+    before each async MSM, with no synchronisation in between, and three MSMs
+    run pipelined; every result is the oracle's MSM of the produced inputs."""
+    import gnark_mi355x as gm
+    n = 1 << 18
+    S0 = gm_ctx.random_scalars("bn254", n, seed=0x71)
+    K = gm_ctx.random_scalars("bn254", n, seed=0x72)
+    P0 = gm_ctx.batch_mul_base("bn254", False, gm.generator("bn254"), K, n)
+    K.free()
+    s_host, p_host = S0.to_host(), P0.to_host()
+    exp = oracle.msm("bn254", False, oracle.fft("bn254", s_host, 0, 0, 0), p_host)
+    bufs = [(gm_ctx.malloc(32 * n), gm_ctx.malloc(64 * n)) for _ in range(3)]
+    try:
+        pend = []
+        for S, P in bufs:
+            S.copy_from(S0)
+            gm_ctx.ntt("bn254", S, n, False, False, False)
+            P.copy_from(P0)
+            pend.append(gm_ctx.msm_async("bn254", S, P, n))
+        assert [p.wait()[1] for p in pend] == [exp] * 3
+    finally:
+        for S, P in bufs:
+            S.free()
+            P.free()
+        S0.free()
+        P0.free()
+
+
 def test_msm_async_inputs_overwritten_in_place(gm_ctx, oracle):
     """A synchronous call queued after gm_msm_async may overwrite the pending
     MSM's scalars and points in place (include/gnark_mi355x.h): the context
