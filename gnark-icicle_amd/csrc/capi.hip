@@ -176,7 +176,9 @@ int gm_destroy(gm_ctx* ctx) {
   for (auto& pr : ctx->pending_reads) hipEventDestroy(pr.second);
   ctx->pending_reads.clear();
   ntt_domains_free(ctx);
-  for (gm::ArenaState* a : {&ctx->arena, &ctx->slots[0], &ctx->slots[1], &ctx->slots[2]}) {
+  std::vector<gm::ArenaState*> arenas{&ctx->arena};
+  for (gm::ArenaState& sa : ctx->slots) arenas.push_back(&sa);
+  for (gm::ArenaState* a : arenas) {
     for (auto& ch : a->chunks) hipFree(ch.base);
     a->chunks.clear();
   }
@@ -217,7 +219,9 @@ int gm_trim(gm_ctx* ctx) {
   for (hipStream_t st : ctx->slot_stream)
     if (st) GM_HIP(hipStreamSynchronize(st));
   if (ctx->g16_stream) GM_HIP(hipStreamSynchronize(ctx->g16_stream));
-  for (gm::ArenaState* a : {&ctx->arena, &ctx->slots[0], &ctx->slots[1], &ctx->slots[2]}) {
+  std::vector<gm::ArenaState*> arenas{&ctx->arena};
+  for (gm::ArenaState& sa : ctx->slots) arenas.push_back(&sa);
+  for (gm::ArenaState* a : arenas) {
     for (auto& ch : a->chunks) hipFree(ch.base);
     a->chunks.clear();
     a->cur_chunk = a->cur_top = 0;
