@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """2^24 plain-key Groth16 proves with host inputs (the icicle.go:204-412 scope), for a
 kernel + memory-copy trace of where the host inputs' cost goes:
-  rocprofv3 --kernel-trace --memory-copy-trace ... -- python3 tools/g16_host_trace.py [stage|async|device]"""
+  rocprofv3 --kernel-trace --memory-copy-trace ... -- python3 tools/g16_host_trace.py [stage|async|device|devonly]"""
 import os
 import sys
 import time
@@ -43,6 +43,17 @@ elif mode == "device":  # device-input proves first (what bench.py times before 
     for _ in range(2):
         dpk.prove_device(W, A, B, C, n, r[:32], r[32:])
 print("mode", mode or "fresh", flush=True)
+if mode == "devonly":  # device-input proves only (for a kernel timeline of the device scope)
+    A, B, C = (ctx.malloc(32 * n) for _ in range(3))
+    for dst, src in zip((A, B, C), srcs):
+        dst.copy_from(src)
+    Wd = W
+    for i in range(3):
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        dpk.prove_device(Wd, A, B, C, n, r[:32], r[32:])
+        print("prove(device inputs) %.1f ms" % ((time.perf_counter() - t0) * 1e3), flush=True)
+    sys.exit(0)
 for i in range(3):
     ctx.synchronize()
     t0 = time.perf_counter()
