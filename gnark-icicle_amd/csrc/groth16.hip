@@ -400,8 +400,17 @@ int pk_upload_ranges(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsigned f
   cp(pk->delta, h->g1_delta, g1b);
   cp(pk->beta2, h->g2_beta, g2b);
   cp(pk->delta2, h->g2_delta, g2b);
+  pk_prepare_h(ctx, pk);
   *out = pk;
   return GM_OK;
+}
+
+void pk_prepare_h(gm_ctx* ctx, const gm_g16_pk* pk) {
+  static const bool on = !getenv("GM_G16_PREPARE_H") || atoi(getenv("GM_G16_PREPARE_H")) != 0;
+  if (!on) return;
+  const int rc = pk->curve == GM_BN254 ? compute_h_prepare<CurveBN254>(ctx, pk->n)
+                                       : compute_h_prepare<CurveBLS12377>(ctx, pk->n);
+  if (rc) (void)hipGetLastError();  // e.g. out of memory: the first prove builds them (or reports it)
 }
 
 namespace {

@@ -50,6 +50,9 @@ int check_curve_id(int curve);
 size_t internal_point_bytes(int curve, bool g2);
 void pk_release(gm_g16_pk* pk);
 void stage_spare_release(gm_g16_pk* pk);  // pk_io.hip
+// computeH's NTT domain and tables for the key's n, built at upload (best effort;
+// GM_G16_PREPARE_H=0 leaves them to the first prove)
+void pk_prepare_h(gm_ctx* ctx, const gm_g16_pk* pk);
 // gnark-layout points on the device -> internal layout at dst (+ window copies)
 int prepare_points_into(gm_ctx* ctx, int curve, bool g2, const void* gnark_dev, size_t count,
                         const MsmPrecomp* pre, void* dst);

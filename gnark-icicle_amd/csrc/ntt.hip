@@ -1115,6 +1115,27 @@ int ntt_domain_prepare(gm_ctx* ctx, size_t n) {
   return get_domain<C>(ctx, logn, &d);
 }
 
+// The domain and the two n-element tables computeH reads (coset powers g^brev(p)
+// and the fused tail's factors), built ahead of the first prove -- at key upload,
+// as the reference generates its twiddles in setupDevicePointers (icicle.go:68-76)
+// -- instead of inside it (2^24: ~15 ms of a first prove's ~25 ms overhead,
+// profiles/r05ae_first_prove.txt).
+template <class C>
+int compute_h_prepare(gm_ctx* ctx, size_t n) {
+  const int logn = log2_exact(n);
+  if (logn < 1 || logn > C::TWO_ADICITY || logn > 30) {
+    set_error("compute_h: n must be a power of two >= 2 within the 2-adicity");
+    return GM_ERR_INVALID;
+  }
+  NttDomain<C>* d;
+  const Fe<typename C::Fr>* t;
+  int rc;
+  if ((rc = get_domain<C>(ctx, logn, &d)) || (rc = domain_table<C>(ctx, d, TAB_G_BREV, &t)) ||
+      (rc = domain_table<C>(ctx, d, TAB_H_POST, &t)))
+    return rc;
+  return GM_OK;
+}
+
 // computeH (prove.go:356-399; icicle.go:453-513), all scalings fused:
 //   a, b, c: INTT (DIF; 1/n folded into the top-pass twiddles) -> bit-reversed
 //            coefficients -> coset NTT (DIT; g^brev(p) applied on load) -> natural
@@ -1182,7 +1203,8 @@ int compute_h_finish(gm_ctx* ctx, void* a, const void* b, const void* c, size_t 
   template int compute_h_finish<C>(gm_ctx*, void*, const void*, const void*, size_t);      \
   template int bitrev_copy_device<C>(gm_ctx*, void*, const void*, size_t);                 \
   template int poly_ops_vec_device<C>(gm_ctx*, void*, const void*, const void*, const void*, size_t); \
-  template int ntt_domain_prepare<C>(gm_ctx*, size_t);
+  template int ntt_domain_prepare<C>(gm_ctx*, size_t);                                           \
+  template int compute_h_prepare<C>(gm_ctx*, size_t);
 GM_NTT_INST(CurveBN254)
 GM_NTT_INST(CurveBLS12377)
 

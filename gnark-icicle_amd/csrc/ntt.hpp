@@ -28,5 +28,8 @@ template <class C>
 int poly_ops_vec_device(gm_ctx* ctx, void* a, const void* b, const void* c, const void* den, size_t n);
 template <class C>
 int ntt_domain_prepare(gm_ctx* ctx, size_t n);
+// the domain and computeH's tables for n, ahead of the first prove (key upload)
+template <class C>
+int compute_h_prepare(gm_ctx* ctx, size_t n);
 void ntt_domains_free(gm_ctx* ctx);
 }  // namespace gm

@@ -478,6 +478,7 @@ int gm_g16_pk_load_cache(gm_ctx* ctx, int fd, gm_g16_pk** out) {
     }
   }
   if (hipStreamSynchronize(ctx->stream) != hipSuccess) return fail(GM_ERR_DEVICE);
+  pk_prepare_h(ctx, pk);
   *out = pk;
   return GM_OK;
 }

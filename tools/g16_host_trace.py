@@ -43,7 +43,15 @@ elif mode == "device":  # device-input proves first (what bench.py times before 
     for _ in range(2):
         dpk.prove_device(W, A, B, C, n, r[:32], r[32:])
 print("mode", mode or "fresh", flush=True)
-if mode == "devonly":  # device-input proves only (for a kernel timeline of the device scope)
+if mode in ("devonly", "devonly_ntt"):  # device-input proves only (devonly_ntt: NTT tables built first)
+    if mode == "devonly_ntt":
+        X = ctx.random_scalars("bn254", n, 3)
+        t0 = time.perf_counter()
+        ctx.ntt("bn254", X, n, False, False, True)
+        ctx.ntt("bn254", X, n, True, True, True)
+        ctx.synchronize()
+        print("ntt tables + 2 transforms %.1f ms" % ((time.perf_counter() - t0) * 1e3), flush=True)
+        X.free()
     A, B, C = (ctx.malloc(32 * n) for _ in range(3))
     for dst, src in zip((A, B, C), srcs):
         dst.copy_from(src)
