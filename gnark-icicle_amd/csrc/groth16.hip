@@ -522,6 +522,43 @@ struct DeviceH : HSource {
   ~DeviceH() override { hipStreamSynchronize(ctx->aux); }
 };
 
+// The context's pinned H2D ring (HostStagedH), created on first use or ahead of
+// it (pk_prepare_h); false when pinned memory or an event is not available (the
+// copies then take the pageable path instead of failing the prove).
+bool h2d_ring_ensure(gm_ctx* ctx) {
+  bool ok = true;
+  for (int i = 0; i < gm_ctx::H2D_SLOTS && ok; i++) {
+    if (!ctx->h2d_pin[i] && hipHostMalloc(&ctx->h2d_pin[i], gm_ctx::H2D_SLOT, hipHostMallocDefault) != hipSuccess) {
+      ctx->h2d_pin[i] = nullptr;
+      ok = false;
+    }
+    if (ok && !ctx->h2d_ev[i] && hipEventCreateWithFlags(&ctx->h2d_ev[i], hipEventDisableTiming) != hipSuccess) {
+      ctx->h2d_ev[i] = nullptr;
+      ok = false;
+    }
+  }
+  (void)hipGetLastError();  // a failed allocation is not the caller's error
+  return ok;
+}
+
+// The context's a / b / c input buffer of host-input proves (gm_ctx::in_abc),
+// grown to 3 n elements.
+int in_abc_reserve(gm_ctx* ctx, size_t n) {
+  const size_t abc = 3 * 32 * n;
+  if (ctx->in_abc_cap >= abc) return GM_OK;
+  void* old = ctx->in_abc;
+  ctx->in_abc = nullptr;  // released below; never left pointing at freed memory
+  ctx->in_abc_cap = 0;
+  if (old) GM_HIP(hipFree(old));
+  if (hipMalloc(&ctx->in_abc, abc) != hipSuccess) {
+    ctx->in_abc = nullptr;
+    set_error("prove: hipMalloc of the a/b/c input buffer failed");
+    return GM_ERR_OOM;
+  }
+  ctx->in_abc_cap = abc;
+  return GM_OK;
+}
+
 // a, b, c in host memory: a helper thread copies them on the context's copy
 // stream (pageable hipMemcpyAsync runs at ~56 GB/s on the box but blocks the
 // calling thread) while the main thread runs the A/B/K MSMs; each vector's
@@ -568,18 +605,7 @@ struct HostStagedH : HSource {
       void* dst[3] = {da, db, dc};
       // the ring is created on first use; when pinned memory (or an event) is not
       // available the copies take the pageable path instead of failing the prove
-      bool ring = pinned;
-      for (int i = 0; i < gm_ctx::H2D_SLOTS && ring && r == GM_OK; i++) {
-        if (!ctx->h2d_pin[i] && hipHostMalloc(&ctx->h2d_pin[i], gm_ctx::H2D_SLOT, hipHostMallocDefault) != hipSuccess) {
-          ctx->h2d_pin[i] = nullptr;
-          ring = false;
-        }
-        if (ring && !ctx->h2d_ev[i] && hipEventCreateWithFlags(&ctx->h2d_ev[i], hipEventDisableTiming) != hipSuccess) {
-          ctx->h2d_ev[i] = nullptr;
-          ring = false;
-        }
-      }
-      (void)hipGetLastError();  // a failed allocation above is not the prove's error
+      const bool ring = pinned && r == GM_OK && h2d_ring_ensure(ctx);
       bool used[gm_ctx::H2D_SLOTS] = {};
       int slot = 0;
       for (int k = 0; k < 3 && r == GM_OK; k++) {
@@ -1246,19 +1272,7 @@ int gm_g16_prove(gm_ctx* ctx, gm_g16_pk* pk, const void* wires, const void* a, c
   int rc;
   if ((rc = w.alloc(arena, 32 * pk->nb_wires))) return rc;
   // a / b / c: the context's input allocation (gm_ctx::in_abc), not the arena
-  const size_t abc = 3 * 32 * pk->n;
-  if (ctx->in_abc_cap < abc) {
-    void* old = ctx->in_abc;
-    ctx->in_abc = nullptr;  // released below; never left pointing at freed memory
-    ctx->in_abc_cap = 0;
-    if (old) GM_HIP(hipFree(old));
-    if (hipMalloc(&ctx->in_abc, abc) != hipSuccess) {
-      ctx->in_abc = nullptr;
-      set_error("prove: hipMalloc of the a/b/c input buffer failed");
-      return GM_ERR_OOM;
-    }
-    ctx->in_abc_cap = abc;
-  }
+  if ((rc = in_abc_reserve(ctx, pk->n))) return rc;
   char* const da = (char*)ctx->in_abc;
   char* const db = da + 32 * pk->n;
   char* const dc = db + 32 * pk->n;
