@@ -28,6 +28,8 @@
 #include "pair_fp2.hpp"
 #include "runtime.hpp"
 
+#include <hip/hip_ext.h>
+
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -1295,7 +1297,7 @@ int msm_launch(gm_ctx* ctx, Arena& arena, const MsmPlan& plan, const void* point
   GM_HIP(hipMemsetAsync(errw.p, 0, 16, st));
   {
     GM_HIP(hipMemsetAsync(buckets.p, 0, sizeof(XYZZ<DF>) * (size_t)t.total, st));  // all-zero XYZZ = infinity
-    ProfScope ps(ctx, G2 ? "msm_accum_g2" : "msm_accum_g1");
+    ProfScope ps(ctx, G2 ? "msm_accum_g2" : "msm_accum_g1", true);  // stamped by the launch
     // G2 defaults to lane pairs; GM_MSM_ACCUM=prefetch|noprefetch selects the
     // one-lane kernels instead (tuning / A-B); for G1, prefetch selects the
     // three-wave prefetching kernel
@@ -1304,10 +1306,10 @@ int msm_launch(gm_ctx* ctx, Arena& arena, const MsmPlan& plan, const void* point
     const bool prefetch = ov && !strcmp(ov, "prefetch");
     if constexpr (PairSel<DF>::ok) {
       if (pair) {
-        hipLaunchKernelGGL(PairSel<DF>::kernel(t.K), dim3(blocks_for(2 * nslices, 128)), dim3(128), 0, st,
-                           reinterpret_cast<const uint32_t*>(points_internal), (uint32_t)plan.npts, plan.keys,
-                           plan.vals, plan.offsets, t.total, t.K, buckets.as<uint32_t>(), pfirst.as<uint32_t>(),
-                           plast.as<uint32_t>(), errw.as<uint32_t>());
+        hipExtLaunchKernelGGL(PairSel<DF>::kernel(t.K), dim3(blocks_for(2 * nslices, 128)), dim3(128), 0, st, ps.a,
+                              ps.b, 0, reinterpret_cast<const uint32_t*>(points_internal), (uint32_t)plan.npts,
+                              plan.keys, plan.vals, plan.offsets, t.total, t.K, buckets.as<uint32_t>(),
+                              pfirst.as<uint32_t>(), plast.as<uint32_t>(), errw.as<uint32_t>());
       }
     } else {
       pair = false;
@@ -1329,10 +1331,10 @@ int msm_launch(gm_ctx* ctx, Arena& arena, const MsmPlan& plan, const void* point
           if (acc_chain && !prefetch && !ov)
             accum = v4 ? k_msm_accum_seg_ch<DF> : k_msm_accum_seg_ch1<DF>;  // v4: K % 4 == 0
         }
-        hipLaunchKernelGGL(accum, dim3(blocks_for(nslices, 128)), dim3(128), 0, st,
-                           reinterpret_cast<const uint32_t*>(points_internal), (uint32_t)plan.npts, plan.keys,
-                           plan.vals, plan.offsets, t.total, t.K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(),
-                           plast.as<XYZZ<DF>>(), errw.as<uint32_t>());
+        hipExtLaunchKernelGGL(accum, dim3(blocks_for(nslices, 128)), dim3(128), 0, st, ps.a, ps.b, 0,
+                              reinterpret_cast<const uint32_t*>(points_internal), (uint32_t)plan.npts, plan.keys,
+                              plan.vals, plan.offsets, t.total, t.K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(),
+                              plast.as<XYZZ<DF>>(), errw.as<uint32_t>());
       }
     }
   }

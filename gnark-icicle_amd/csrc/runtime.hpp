@@ -120,19 +120,24 @@ struct gm_ctx {
 namespace gm {
 
 // Records a kernel launch bracketed by events when profiling is enabled.
+// kernel = true: the events are not recorded on the stream; the scope's one
+// kernel is launched with hipExtLaunchKernelGGL(..., a, b, ...), which stamps
+// them with the kernel's own start and end (its execution, not the time it
+// waited in the queue for wave slots another stream's kernels held).
 struct ProfScope {
   gm_ctx* ctx;
   const char* name;
+  bool kernel;
   hipEvent_t a = nullptr, b = nullptr;
-  ProfScope(gm_ctx* c, const char* n) : ctx(c), name(n) {
+  ProfScope(gm_ctx* c, const char* n, bool k = false) : ctx(c), name(n), kernel(k) {
     if (!ctx->profiling) return;
     a = take();
     b = take();
-    hipEventRecord(a, ctx->stream);
+    if (!kernel) hipEventRecord(a, ctx->stream);
   }
   ~ProfScope() {
     if (!ctx->profiling) return;
-    hipEventRecord(b, ctx->stream);
+    if (!kernel) hipEventRecord(b, ctx->stream);
     ctx->pending.push_back({name, a, b});
   }
   hipEvent_t take() {
