@@ -236,6 +236,10 @@ def main():
                           "traffic_streaming_corrected = 2 x FETCH + WRITE (the guide's streaming factor); committed "
                           "profile of this kernel, not measured in this run)",
         "avg_launch_ms": round(acc_avg_ms, 4),
+        "timing": "hipExtLaunchKernelGGL start / stop events of every accumulation launch in the timed loop "
+                  "(csrc/msm_impl.hpp); without a profiler attached the start stamp can precede the first wave "
+                  "while the launch waits for wave slots the neighbouring MSMs' kernels hold (under rocprofv3 the "
+                  "same events give the kernel-trace duration, profiles/r05ag_accum_event_timing.txt)",
         "bytes_per_launch": alg_bytes,
         "int_alu": {"achieved": round(tmads, 3), "peak": round(MAD_PEAK_T, 2), "unit": "T v_mad_u64_u32/s",
                     "frac": round(tmads / MAD_PEAK_T, 4),
