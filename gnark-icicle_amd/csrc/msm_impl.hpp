@@ -781,10 +781,17 @@ struct PairSel<Fe2<P, B>> {
     static const char* wpe = getenv("GM_MSM_PAIR_WPE");
     static const bool v4env = !getenv("GM_MSM_ACC_V4") || atoi(getenv("GM_MSM_ACC_V4")) != 0;
     const bool v4 = v4env && (K & 3) == 0;
-    const bool on = pf ? pf[0] != '0' : P::N <= 9;
+    // BN254 default since r05: one mad chain per product (fe_mul CHAIN) in the pair
+    // add, no prefetch, three waves per SIMD (168 VGPRs, no spill; the prefetching
+    // kernel needs 200 and runs two): G2 2^20 accumulation 3.91-3.92 -> 3.86-3.89 ms,
+    // Groth16 2^24 148.0-149.3 -> 146.8-147.8 ms (profiles/r05aj_pair_chain_ab.txt).
+    // GM_MSM_PAIR_CHAIN=0 (or GM_MSM_PAIR_PF set): the kernels below.
+    static const bool pch = !getenv("GM_MSM_PAIR_CHAIN") || atoi(getenv("GM_MSM_PAIR_CHAIN")) != 0;
     if constexpr (P::N <= 9) {
       if (wpe && wpe[0] == '3') return k_msm_accum_seg_pair<P, B, false, 3>;
+      if (v4 && pch && !pf) return k_msm_accum_seg_pair<P, B, false, 3, true, true>;
     }
+    const bool on = pf ? pf[0] != '0' : P::N <= 9;
     if (v4)
       return on ? k_msm_accum_seg_pair<P, B, true, GM_PAIR_WPE, true>
                 : k_msm_accum_seg_pair<P, B, false, GM_PAIR_WPE, true>;

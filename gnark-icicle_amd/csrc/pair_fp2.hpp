@@ -52,7 +52,7 @@ GM_DEV Fe<P> fe_select(bool c, const Fe<P>& a, const Fe<P>& b) {
 // instructions: no per-lane sign select in every column, no + p pass and no
 // final conditional subtraction (the sum is < (16 + 20) p^2 / R' + p < 1.22p
 // for BN254, R' / p ~ 169).
-template <class P, int BETA>
+template <class P, int BETA, bool CH = false>
 GM_DEV Fe<P> pf2_mul(const Fe<P>& a, const Fe<P>& b) {
   static_assert(BETA == -1 || BETA == -5, "unsupported non-residue");
   const bool odd = pair_odd();
@@ -62,7 +62,7 @@ GM_DEV Fe<P> pf2_mul(const Fe<P>& a, const Fe<P>& b) {
     const Fe<P> b5 = fe_times5_lz(bp);  // < 20p, normalised limbs
     y2 = fe_select(odd, b, b5);
   }
-  return fe_mul2_redc_u(a, fe_select(odd, bp, b), fe_select(odd, ap, fe_negk_cf<5>(ap)), y2);
+  return fe_mul2_redc_u<P, CH>(a, fe_select(odd, bp, b), fe_select(odd, ap, fe_negk_cf<5>(ap)), y2);
 }
 
 // x1 y1 + x2 y2 - x3 y3 - x4 y4 + p in ONE Montgomery reduction (signed columns:
@@ -122,7 +122,7 @@ GM_DEV Fe<P> pf2_mul_sub(const Fe<P>& R, const Fe<P>& W, const Fe<P>& Y, const F
 }
 
 // Component of a^2, inputs < IN p per component, result < 2p.
-template <class P, int BETA, int IN>
+template <class P, int BETA, int IN, bool CH = false>
 GM_DEV Fe<P> pf2_sqr(const Fe<P>& a) {
   if constexpr (BETA == -1) {
     static_assert(IN <= 4, "pf2_sqr output bound (< 2p) needs inputs < 4p");
@@ -133,9 +133,9 @@ GM_DEV Fe<P> pf2_sqr(const Fe<P>& a) {
     const Fe<P> v = odd ? ap : fe_sub_lz<IN>(a, ap);
     // u < 2 IN p, v < 2 IN p: (2 IN p)^2 / R' + p < 1.4p for IN <= 4 (BN254
     // R' / p ~ 169): already below 2p, no conditional subtraction
-    return fe_mul_lz(u, v);
+    return fe_mul<P, false, CH>(u, v);
   } else {
-    return pf2_mul<P, BETA>(a, a);
+    return pf2_mul<P, BETA, CH>(a, a);
   }
 }
 
@@ -190,7 +190,8 @@ GM_DEV PXYZZ<P> pxyzz_dbl_aff(const Fe<P>& px, const Fe<P>& py) {
 // ms).  BLS12-377 keeps y negated up front and three chains: its 14-limb add
 // already spills at three waves per SIMD, and the trimmed form spilled more
 // (171 -> 185 VGPRs, 2^22 accumulation 46.5 -> 47.4 ms; profiles/r03e_ab.txt).
-template <class P, int BETA>
+// CH: one mad chain per product (fe_mul CHAIN) in the add's products
+template <class P, int BETA, bool CH = false>
 GM_DEV void pxyzz_add_aff(PXYZZ<P>& a, const Fe<P>& px, const Fe<P>& py_in, bool neg) {
   static_assert(P::BITS + 7 <= RADIX * P::N, "lazy reduction needs R' > 128 p");
   constexpr bool TRIM = P::N <= 9;
@@ -206,29 +207,29 @@ GM_DEV void pxyzz_add_aff(PXYZZ<P>& a, const Fe<P>& px, const Fe<P>& py_in, bool
     a.zzz = a.zz;
     return;
   }
-  const Fe<P> Pd = fe_sub_lz<2>(pf2_mul<P, BETA>(px, a.zz), a.x);    // U2 - X1   < 4p
+  const Fe<P> Pd = fe_sub_lz<2>(pf2_mul<P, BETA, CH>(px, a.zz), a.x);    // U2 - X1   < 4p
   Fe<P> R;                                                          // +-S2 - Y1 < 4p
   if constexpr (TRIM) {
     // S2 < 2p; 2p - S2 in (0, 2p]
-    R = fe_sub_lz<2>(fe_cneg2p_cf(pf2_mul<P, BETA>(py, a.zzz), neg), a.y);
+    R = fe_sub_lz<2>(fe_cneg2p_cf(pf2_mul<P, BETA, CH>(py, a.zzz), neg), a.y);
   } else {
-    R = fe_sub_lz<2>(pf2_mul<P, BETA>(py, a.zzz), a.y);
+    R = fe_sub_lz<2>(pf2_mul<P, BETA, CH>(py, a.zzz), a.y);
   }
   if (pair_all(fe_is_zero_lz<4>(Pd))) {
     if (pair_all(fe_is_zero_lz<4>(R))) a = pxyzz_dbl_aff<P, BETA>(px, (TRIM && neg) ? fe_neg(py) : py);
     else a = pxyzz_inf<P>();
     return;
   }
-  const Fe<P> PP = pf2_sqr<P, BETA, 4>(Pd);                         // < 2p
-  const Fe<P> PPP = pf2_mul<P, BETA>(Pd, PP);                       // < 2p
-  a.zz = pf2_mul<P, BETA>(a.zz, PP);
-  const Fe<P> Q = pf2_mul<P, BETA>(a.x, PP);                        // < 2p
-  a.zzz = pf2_mul<P, BETA>(a.zzz, PPP);
+  const Fe<P> PP = pf2_sqr<P, BETA, 4, CH>(Pd);                     // < 2p
+  const Fe<P> PPP = pf2_mul<P, BETA, CH>(Pd, PP);                   // < 2p
+  a.zz = pf2_mul<P, BETA, CH>(a.zz, PP);
+  const Fe<P> Q = pf2_mul<P, BETA, CH>(a.x, PP);                    // < 2p
+  a.zzz = pf2_mul<P, BETA, CH>(a.zzz, PPP);
   Fe<P> X3;                                                         // < 8p
   if constexpr (TRIM) {
-    X3 = fe_sub2x_lz<6>(pf2_sqr<P, BETA, 4>(R), PPP, Q);
+    X3 = fe_sub2x_lz<6>(pf2_sqr<P, BETA, 4, CH>(R), PPP, Q);
   } else {
-    X3 = fe_sub_lz<4>(fe_sub_lz<2>(pf2_sqr<P, BETA, 4>(R), PPP), fe_add_lz(Q, Q));
+    X3 = fe_sub_lz<4>(fe_sub_lz<2>(pf2_sqr<P, BETA, 4, CH>(R), PPP), fe_add_lz(Q, Q));
   }
   fe_to2p<8>(X3);
   Fe<P> Y3;
@@ -237,7 +238,7 @@ GM_DEV void pxyzz_add_aff(PXYZZ<P>& a, const Fe<P>& px, const Fe<P>& py_in, bool
     //   lane 0: R0 W0 + Y1 P1 - R1 W1 - Y0 P0     lane 1: R1 W0 + R0 W1 - Y1 P0 - Y0 P1
     Y3 = pf2_mul_sub(R, fe_sub_lz<2>(Q, X3), a.y, PPP);  // < 2.3p
   } else {
-    Y3 = fe_sub_lz<2>(pf2_mul<P, BETA>(R, fe_sub_lz<2>(Q, X3)), pf2_mul<P, BETA>(a.y, PPP));  // < 4p
+    Y3 = fe_sub_lz<2>(pf2_mul<P, BETA, CH>(R, fe_sub_lz<2>(Q, X3)), pf2_mul<P, BETA, CH>(a.y, PPP));  // < 4p
   }
   fe_to2p<4>(Y3);
   a.x = X3;
@@ -284,7 +285,7 @@ GM_DEV PairPt<P> pair_load_pt(const uint32_t* __restrict__ pt) {
 // PF: prefetch the next point's components (2 x NG registers) while the
 // current add runs; without it the other waves hide the load (GM_MSM_PAIR_PF=0).
 // WPE: waves-per-SIMD floor for the register allocator (1 = no cap).
-template <class P, int BETA, bool PF = true, int WPE = GM_PAIR_WPE, bool V4 = false>
+template <class P, int BETA, bool PF = true, int WPE = GM_PAIR_WPE, bool V4 = false, bool CH = false>
 __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_msm_accum_seg_pair(const uint32_t* __restrict__ points, uint32_t n,
                                                             const uint32_t* __restrict__ keys,
@@ -366,7 +367,7 @@ k_msm_accum_seg_pair(const uint32_t* __restrict__ points, uint32_t n,
     }
     const Fe<P> px = fe_unpack<P>(pt.x);
     const Fe<P> py = fe_unpack<P>(pt.y);
-    pxyzz_add_aff<P, BETA>(acc, px, py, (v >> 31) != 0);
+    pxyzz_add_aff<P, BETA, CH>(acc, px, py, (v >> 31) != 0);
     v = vn;
     if (PF) pt = ptn;
   }
