@@ -118,7 +118,7 @@ GM_DEV void xyzz_add_aff(XYZZ<F>& a, const Affine<F>& p) {
 // and X3 = R^2 - PPP - 2Q takes one borrow chain (fe_sub2x_lz).
 // CH: one dependent mad chain per product (fe_mul CHAIN) -- A/B variant of the
 // accumulation kernel only (GM_MSM_ACC_CHAIN=1).
-template <class P, bool CH = false>
+template <class P, int CH = 0>
 GM_DEV void xyzz_add_aff_lz(XYZZ<Fe<P>>& a, const Affine<Fe<P>>& p, bool neg) {
   static_assert(P::BITS + 7 <= RADIX * P::N, "lazy reduction needs R' > 128 p");
   using F = Fe<P>;

@@ -271,7 +271,18 @@ GM_DEV Fe<P> fe_neg(const Fe<P>& a) {
 #ifndef GM_FE_CHAIN
 #define GM_FE_CHAIN 0
 #endif
-template <class P, bool REDUCE = true, bool CHAIN = GM_FE_CHAIN>
+// CHAIN levels of the products below: 0 -- the compiler's schedule; 1 -- one
+// mad chain per column (a register barrier between columns); 2 -- strict: every
+// mad takes the previous one's result as its addend (a barrier after each), so
+// no column is summed in a second register pair and joined with a 64-bit add
+// (v_lshl_add_u64), and squarings double an operand instead of shifting the
+// cross sum.  Level 2 costs one wait state per dependent mad (s_nop 0, hidden by
+// the other waves).
+#define GM_STRICT_STEP(acc, CH) \
+  do {                              \
+    if constexpr ((CH) >= 2) __asm__ volatile("" : "+v"(acc)); \
+  } while (0)
+template <class P, bool REDUCE = true, int CHAIN = GM_FE_CHAIN>
 GM_DEV Fe<P> fe_mul(const Fe<P>& a, const Fe<P>& b) {
   constexpr int N = P::N;
   uint32_t m[N];
@@ -283,11 +294,15 @@ GM_DEV Fe<P> fe_mul(const Fe<P>& a, const Fe<P>& b) {
       if (k) __asm__ volatile("" : "+v"(acc));
     }
 #pragma unroll
-    for (int i = (k - N + 1 > 0 ? k - N + 1 : 0); i <= (k < N - 1 ? k : N - 1); i++)
+    for (int i = (k - N + 1 > 0 ? k - N + 1 : 0); i <= (k < N - 1 ? k : N - 1); i++) {
       acc += (uint64_t)a.v[i] * b.v[k - i];
+      GM_STRICT_STEP(acc, CHAIN);
+    }
 #pragma unroll
-    for (int i = (k - N + 1 > 0 ? k - N + 1 : 0); i <= (k - 1 < N - 1 ? k - 1 : N - 1); i++)
+    for (int i = (k - N + 1 > 0 ? k - N + 1 : 0); i <= (k - 1 < N - 1 ? k - 1 : N - 1); i++) {
       acc += (uint64_t)m[i] * P::p(k - i);
+      GM_STRICT_STEP(acc, CHAIN);
+    }
     if (k < N) {
       m[k] = ((uint32_t)acc * P::INV) & LIMB_MASK;
       acc += (uint64_t)m[k] * P::p(0);
@@ -302,7 +317,7 @@ GM_DEV Fe<P> fe_mul(const Fe<P>& a, const Fe<P>& b) {
 }
 
 // Squaring: the symmetric products a_i a_j (i != j) are formed once and doubled.
-template <class P, bool REDUCE = true, bool CHAIN = GM_FE_CHAIN>
+template <class P, bool REDUCE = true, int CHAIN = GM_FE_CHAIN>
 GM_DEV Fe<P> fe_sqr(const Fe<P>& a) {
   constexpr int N = P::N;
   uint32_t m[N];
@@ -313,17 +328,34 @@ GM_DEV Fe<P> fe_sqr(const Fe<P>& a) {
     if constexpr (CHAIN) {
       if (k) __asm__ volatile("" : "+v"(acc));
     }
-    uint64_t cross = 0;
+    if constexpr (CHAIN >= 2) {
+      // 2 a_i a_j as a_i (2 a_j): 2 a_j < 2^30, the column stays below 2^64
 #pragma unroll
-    for (int i = (k - N + 1 > 0 ? k - N + 1 : 0); i <= (k < N - 1 ? k : N - 1); i++) {
-      const int j = k - i;
-      if (i < j) cross += (uint64_t)a.v[i] * a.v[j];
+      for (int i = (k - N + 1 > 0 ? k - N + 1 : 0); i <= (k < N - 1 ? k : N - 1); i++) {
+        const int j = k - i;
+        if (i < j) {
+          acc += (uint64_t)a.v[i] * (a.v[j] << 1);
+          GM_STRICT_STEP(acc, CHAIN);
+        }
+      }
+    } else {
+      uint64_t cross = 0;
+#pragma unroll
+      for (int i = (k - N + 1 > 0 ? k - N + 1 : 0); i <= (k < N - 1 ? k : N - 1); i++) {
+        const int j = k - i;
+        if (i < j) cross += (uint64_t)a.v[i] * a.v[j];
+      }
+      acc += cross << 1;
     }
-    acc += cross << 1;
-    if ((k & 1) == 0) acc += (uint64_t)a.v[k / 2] * a.v[k / 2];
+    if ((k & 1) == 0) {
+      acc += (uint64_t)a.v[k / 2] * a.v[k / 2];
+      GM_STRICT_STEP(acc, CHAIN);
+    }
 #pragma unroll
-    for (int i = (k - N + 1 > 0 ? k - N + 1 : 0); i <= (k - 1 < N - 1 ? k - 1 : N - 1); i++)
+    for (int i = (k - N + 1 > 0 ? k - N + 1 : 0); i <= (k - 1 < N - 1 ? k - 1 : N - 1); i++) {
       acc += (uint64_t)m[i] * P::p(k - i);
+      GM_STRICT_STEP(acc, CHAIN);
+    }
     if (k < N) {
       m[k] = ((uint32_t)acc * P::INV) & LIMB_MASK;
       acc += (uint64_t)m[k] * P::p(0);
@@ -383,7 +415,7 @@ GM_DEV Fe<P> fe_sqr_lz(const Fe<P>& a) { return fe_sqr<P, false>(a); }
 // lane-pair Fp2 product, whose two lanes then run the same instructions.  Column bound:
 // N (2^58 + 2^59 + 2^58) < 2^64 for N <= 14 with x1, y1, y2 normalised and x2
 // limbs < 2^30.  Output < (x1 y1 + x2 y2) / R' + p, limbs normalised.
-template <class P, bool CHAIN = GM_FE_CHAIN>
+template <class P, int CHAIN = GM_FE_CHAIN>
 GM_DEV Fe<P> fe_mul2_redc_u(const Fe<P>& x1, const Fe<P>& y1, const Fe<P>& x2, const Fe<P>& y2) {
   constexpr int N = P::N;
   static_assert(N <= 14, "unsigned two-product column bound");
@@ -398,11 +430,15 @@ GM_DEV Fe<P> fe_mul2_redc_u(const Fe<P>& x1, const Fe<P>& y1, const Fe<P>& x2, c
 #pragma unroll
     for (int i = (k - N + 1 > 0 ? k - N + 1 : 0); i <= (k < N - 1 ? k : N - 1); i++) {
       acc += (uint64_t)x1.v[i] * y1.v[k - i];
+      GM_STRICT_STEP(acc, CHAIN);
       acc += (uint64_t)x2.v[i] * y2.v[k - i];
+      GM_STRICT_STEP(acc, CHAIN);
     }
 #pragma unroll
-    for (int i = (k - N + 1 > 0 ? k - N + 1 : 0); i <= (k - 1 < N - 1 ? k - 1 : N - 1); i++)
+    for (int i = (k - N + 1 > 0 ? k - N + 1 : 0); i <= (k - 1 < N - 1 ? k - 1 : N - 1); i++) {
       acc += (uint64_t)m[i] * P::p(k - i);
+      GM_STRICT_STEP(acc, CHAIN);
+    }
     if (k < N) {
       m[k] = ((uint32_t)acc * P::INV) & LIMB_MASK;
       acc += (uint64_t)m[k] * P::p(0);

@@ -321,7 +321,7 @@ GM_DEV Fe<P> ntt_tw(const Fe<P>* __restrict__ sub, int i) {
 // below a + K p with K one above fe_sub_lz's, every product input < 33 p^2 < R' p).
 #define MUL(x, y) (CH ? fe_mul_lz_chain(x, y) : fe_mul_lz(x, y))
 // DIF radix-2 butterfly pair of one round: (u, v) -> (u + v, (u - v + Kp) w)
-template <class P, bool CH>
+template <class P, int CH>
 GM_DEV void r4_dif(Fe<P> (&e)[4], const Fe<P>& t1, const Fe<P>& t2, const Fe<P>& t3) {
   // stage lm: (e0, e2) by w_2m^jj, (e1, e3) by w_2m^(jj+s); inputs < 2p
   const Fe<P> s0 = fe_add_lz(e[0], e[2]);                        // < 4p
@@ -338,7 +338,7 @@ GM_DEV void r4_dif(Fe<P> (&e)[4], const Fe<P>& t1, const Fe<P>& t2, const Fe<P>&
   e[3] = MUL(fe_sub_cf<3>(d0, d1), t3);                    // < 2p
 }
 // the s = 1 DIF round (twiddles 1, w_4, 1): inputs < 2p, outputs < 8p
-template <class P, bool CH>
+template <class P, int CH>
 GM_DEV void r4_dif_w4(Fe<P> (&e)[4], const Fe<P>& w4) {
   const Fe<P> s0 = fe_add_lz(e[0], e[2]);                        // < 4p
   const Fe<P> d0 = fe_sub_lz<2>(e[0], e[2]);                     // < 4p
@@ -355,7 +355,7 @@ GM_DEV void r4_dif_w4(Fe<P> (&e)[4], const Fe<P>& w4) {
 // the products (< 2p) reset the other lanes.  The last (w_4) round's outputs,
 // < 64p at t = 8, go straight into the inter-pass twiddle product of the store
 // (64 p^2 < R' p).
-template <class P, bool CH, int B>
+template <class P, int CH, int B>
 GM_DEV void r4_dif_grow(Fe<P> (&e)[4], const Fe<P>& t1, const Fe<P>& t2, const Fe<P>& t3) {
   const Fe<P> s0 = fe_add_lz(e[0], e[2]);                        // < 2B p
   const Fe<P> d0 = MUL(fe_sub_cf<B + 1>(e[0], e[2]), t1);        // < 2p
@@ -367,7 +367,7 @@ GM_DEV void r4_dif_grow(Fe<P> (&e)[4], const Fe<P>& t1, const Fe<P>& t2, const F
   e[2] = fe_add_lz(d0, d1);                                      // < 4p
   e[3] = MUL(fe_sub_cf<3>(d0, d1), t3);                          // < 2p
 }
-template <class P, bool CH, int B>
+template <class P, int CH, int B>
 GM_DEV void r4_dif_w4_grow(Fe<P> (&e)[4], const Fe<P>& w4) {
   const Fe<P> s0 = fe_add_lz(e[0], e[2]);                        // < 2B p
   const Fe<P> d0 = fe_sub_lz<B>(e[0], e[2]);                     // < 2B p
@@ -379,7 +379,7 @@ GM_DEV void r4_dif_w4_grow(Fe<P> (&e)[4], const Fe<P>& w4) {
   e[3] = fe_sub_lz<2>(d0, d1);                                   // < (2B + 2) p
 }
 // DIT (Harvey) round: (u, v) -> (u + v w, u - v w + 2p); inputs < 4p, outputs < 4p
-template <class P, bool CH>
+template <class P, int CH>
 GM_DEV void r4_dit(Fe<P> (&e)[4], const Fe<P>& a, const Fe<P>& b, const Fe<P>& c) {
   // stage lm: (e0, e1), (e2, e3) by w_2m^jj
   fe_reduce_k<2>(e[0]);
@@ -401,7 +401,7 @@ GM_DEV void r4_dit(Fe<P> (&e)[4], const Fe<P>& a, const Fe<P>& b, const Fe<P>& c
   e[3] = fe_sub_lz<2>(s1, y);
 }
 // the s = 1 DIT round (twiddles 1, 1, w_4): inputs < 2p, outputs < 4p
-template <class P, bool CH>
+template <class P, int CH>
 GM_DEV void r4_dit_w4(Fe<P> (&e)[4], const Fe<P>& w4) {
   const Fe<P> s0 = fe_add_lz(e[0], e[1]);                        // < 4p
   const Fe<P> s1 = fe_sub_lz<2>(e[0], e[1]);                     // < 4p
@@ -418,7 +418,7 @@ GM_DEV void r4_dit_w4(Fe<P> (&e)[4], const Fe<P>& w4) {
 // < 8p; a generic round takes < B p and leaves < (B + 4) p (products < 2p, every
 // product input below 19p); the store brings the < 20p (t = 8) outputs below 4p
 // with three subtractions per element instead of four per round.
-template <class P, bool CH>
+template <class P, int CH>
 GM_DEV void r4_dit_grow(Fe<P> (&e)[4], const Fe<P>& a, const Fe<P>& b, const Fe<P>& c) {
   const Fe<P> v1 = MUL(e[1], a);                                 // < 2p
   const Fe<P> v3 = MUL(e[3], a);
@@ -432,7 +432,7 @@ GM_DEV void r4_dit_grow(Fe<P> (&e)[4], const Fe<P>& a, const Fe<P>& b, const Fe<
   e[1] = fe_add_lz(s1, y);
   e[3] = fe_sub_lz<2>(s1, y);
 }
-template <class P, bool CH>
+template <class P, int CH>
 GM_DEV void r4_dit_w4_grow(Fe<P> (&e)[4], const Fe<P>& w4) {
   const Fe<P> s0 = fe_add_lz(e[0], e[1]);                        // < 4p
   const Fe<P> s1 = fe_sub_lz<2>(e[0], e[1]);                     // < 4p
@@ -464,7 +464,7 @@ GM_DEV void r4_fetch_tw(const Fe<P>* __restrict__ sub, int t, int ls, int k, Fe<
   }
 }
 
-template <class P, bool DIT, bool CH = false>
+template <class P, bool DIT, int CH = 0>
 __global__ void __launch_bounds__(NTT_TPB) __attribute__((amdgpu_waves_per_eu(DIT ? (std::is_same<P, Bn254Fr>::value ? NTT_DIT_WPE_BN254 : NTT_R4_WPE) : NTT_DIF_WPE))) k_ntt_pass4(Fe<P>* __restrict__ data, int logn, int lo, int t, int grow_mask,
                                                        const Fe<P>* __restrict__ tw,
                                                        const Fe<P>* __restrict__ sub,
@@ -970,9 +970,11 @@ static int run_passes(gm_ctx* ctx, NttDomain<C>* d, Fe<typename C::Fr>* a, bool 
   static const bool swg = getenv("GM_NTT_SWG") ? atoi(getenv("GM_NTT_SWG")) != 0 : true;
   // radix-4 passes (k_ntt_pass4) by default; GM_NTT_R4=0: the radix-2 kernel (A/B)
   static const bool r4 = getenv("GM_NTT_R4") ? atoi(getenv("GM_NTT_R4")) != 0 : true;
-  // one dependent mad chain per product (fe_mul CHAIN: the compiler otherwise sums
-  // each column in two halves and adds them, v_lshl_add_u64 per column; 2.20-2.23
-  // -> 2.10-2.12 ms per 2^24 transform, profiles/r04h_ntt_ab.txt); GM_NTT_CHAIN=0: A/B
+  // strict mad chains in every product (fe_mul CHAIN level 2: each mad adds onto the
+  // previous one, no column summed in halves and joined with v_lshl_add_u64; per-
+  // column chains (level 1, r04) took 2.20-2.23 -> 2.10-2.12 ms per 2^24 transform,
+  // profiles/r04h_ntt_ab.txt, strict ones 2.11 -> 2.05-2.06, r05an_strict_chain_ab.txt);
+  // GM_NTT_CHAIN=0: the compiler's schedule (A/B)
   static const bool r4chain = getenv("GM_NTT_CHAIN") ? atoi(getenv("GM_NTT_CHAIN")) != 0 : true;
   // growing bounds: bit 0 DIF passes (r4_dif_grow), bit 1 DIT passes (r4_dit_grow)
   static const int r4grow = getenv("GM_NTT_GROW") ? atoi(getenv("GM_NTT_GROW")) : 3;
@@ -990,8 +992,8 @@ static int run_passes(gm_ctx* ctx, NttDomain<C>* d, Fe<typename C::Fr>* a, bool 
     const unsigned grid = (unsigned)((nother + B - 1) / B);
     ProfScope pscope(ctx, "ntt_pass");
     if (r4 && ps.t >= 2) {
-      auto k4 = dit ? (r4chain ? k_ntt_pass4<Fr, true, true> : k_ntt_pass4<Fr, true>)
-                    : (r4chain ? k_ntt_pass4<Fr, false, true> : k_ntt_pass4<Fr, false>);
+      auto k4 = dit ? (r4chain ? k_ntt_pass4<Fr, true, 2> : k_ntt_pass4<Fr, true>)
+                    : (r4chain ? k_ntt_pass4<Fr, false, 2> : k_ntt_pass4<Fr, false>);
       hipLaunchKernelGGL(k4, dim3(grid), dim3(NTT_TPB),
                          sizeof(Fe<Fr>) * NTT_TILE, st, a, d->logn, ps.lo, ps.t, r4grow, tw, sub, first ? fz.pre : nullptr,
                          last ? fz.post : nullptr, first ? fz.pb : nullptr, first ? fz.pc : nullptr);

@@ -15,6 +15,6 @@ mkdir -p "$(dirname "$OUT")" && export TMPDIR=/tmp
 for rep in $(seq 1 "$REPS"); do
   for v in "${VARIANTS[@]}"; do
     res=$(env $v timeout -k 10 "${AB_TIMEOUT:-300}" "$@" 2>> "$OUT.err") || { echo "failed: [$v] $*" >&2; tail -20 "$OUT.err" >&2; exit 1; }
-    echo "$res" | sed "s|^|[${v:-default}] rep $rep | " | tee -a "$OUT"
+    echo "$res" | sed "s%^%[${v:-default}] rep $rep | %" | tee -a "$OUT"
   done
 done
