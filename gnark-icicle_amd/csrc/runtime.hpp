@@ -250,7 +250,12 @@ inline void par_memcpy(void* dst, const void* src, size_t len, int nt) {
   std::vector<std::thread> ws;
   for (int i = 1; i < nt && (size_t)i * part < len; i++) {
     const size_t o = (size_t)i * part;
-    ws.emplace_back([=] { memcpy((char*)dst + o, (const char*)src + o, std::min(part, len - o)); });
+    try {
+      ws.emplace_back([=] { memcpy((char*)dst + o, (const char*)src + o, std::min(part, len - o)); });
+    } catch (...) {  // no thread to be had: this thread copies the remainder itself
+      memcpy((char*)dst + o, (const char*)src + o, len - o);
+      break;
+    }
   }
   memcpy(dst, src, std::min(part, len));
   for (auto& w : ws) w.join();
