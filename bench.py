@@ -45,8 +45,8 @@ G16_BYTES_PER_ELEM = 4 * 96 + 160 + 7 * 64 + 128
 # committed rocprofv3 --pmc summaries the roofline's traffic / valu fields are
 # read from (collected by tools/gpu_pmc.sh / tools/pmc_traffic.py on the bench's
 # own MSM workload; NOT measured inside this run)
-PMC_TRAFFIC_FILE = "profiles/r05j_pmc_traffic.json"
-PMC_VALU_FILE = "profiles/r05j_pmc_valu.json"
+PMC_TRAFFIC_FILE = "profiles/r05ar_pmc_traffic.json"
+PMC_VALU_FILE = "profiles/r05ar_pmc_valu.json"
 ACCUM_KERNEL = "k_msm_accum_seg_ch"  # the default BN254 G1 accumulation (msm_impl.hpp)
 
 
