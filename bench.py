@@ -105,11 +105,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # torch first (its import does not initialise HIP, and its HIP runtime must be
-    # the process's first), then the library, before anything initialises HIP: the
-    # library's load-time constructor gives the process 8 hardware queues unless
-    # GPU_MAX_HW_QUEUES is already set (csrc/capi.hip), so the in-flight MSMs'
-    # streams overlap -- the bench sets nothing itself, exactly as a gnark process
-    # calling the Go hook.
+    # the process's first), then the library.  The bench sets no HIP environment
+    # itself, exactly as a gnark process calling the Go hook.
     import torch
     import gnark_mi355x as gm
     hwq_preset = os.environ.get("GPU_MAX_HW_QUEUES")
@@ -213,9 +210,17 @@ def main():
     # ---- roofline of the dominant kernel (bucket accumulation) ------------------
     acc_ms, acc_cnt = stats.get("msm_accum_g1", (0.0, 0))
     acc_avg_ms = acc_ms / max(acc_cnt, 1)
+    # A launch time above the step time cannot be the kernel's own run time (the
+    # launches would overlap each other): such a figure is not a kernel time and
+    # is not priced; the isolated launch (the same kernel with the chip to itself)
+    # is used instead and the line says so.
+    pipelined_ok = 0 < acc_avg_ms <= ms_per_step
+    pipelined_avg_ms = acc_avg_ms
+    if not pipelined_ok:
+        acc_avg_ms = iso_avg_ms
     alg_bytes = MSM_BYTES_PER_POINT * n  # per launch: one MSM of n points
     achieved_gbs = alg_bytes / (acc_avg_ms * 1e-3) / 1e9 if acc_avg_ms > 0 else 0.0
-    glv = os.environ.get("GM_MSM_GLV", "1")[:1] != "0"  # BN254 GLV split (msm_impl.hpp GlvBn254)
+    glv = n <= (1 << 21)  # BN254 GLV split up to 2^21 points (capi.hip msm_glv_on)
     npts = 2 * n if glv else n                      # virtual points: P_i and phi(P_i)
     c = max(8, min(20, npts.bit_length() - 1 - 4))  # gm choose_window
     windows = -(-128 // c) if glv else -(-255 // c)  # ceil((bits + 1) / c), bits = 127 / 254
@@ -236,10 +241,13 @@ def main():
                           "traffic_streaming_corrected = 2 x FETCH + WRITE (the guide's streaming factor); committed "
                           "profile of this kernel, not measured in this run)",
         "avg_launch_ms": round(acc_avg_ms, 4),
-        "timing": "hipExtLaunchKernelGGL start / stop events of every accumulation launch in the timed loop "
-                  "(csrc/msm_impl.hpp); without a profiler attached the start stamp can precede the first wave "
-                  "while the launch waits for wave slots the neighbouring MSMs' kernels hold (under rocprofv3 the "
-                  "same events give the kernel-trace duration, profiles/r05ag_accum_event_timing.txt)",
+        "timing": ("hipExtLaunchKernelGGL start / stop events of every accumulation launch in the timed loop "
+                   "(csrc/msm_impl.hpp); the in-flight MSMs' accumulations run one after another "
+                   "(gm_ctx::acc_tail), so each bracket is one kernel's own run, beside the other MSMs' sorts "
+                   "and reductions" if pipelined_ok else
+                   "the timed loop's launch average (%.4f ms) exceeds ms_per_step, so it is not a kernel time: "
+                   "avg_launch_ms / achieved / frac are the isolated launch's (below)" % pipelined_avg_ms),
+        "timing_source": "pipelined" if pipelined_ok else "isolated",
         "bytes_per_launch": alg_bytes,
         "int_alu": {"achieved": round(tmads, 3), "peak": round(MAD_PEAK_T, 2), "unit": "T v_mad_u64_u32/s",
                     "frac": round(tmads / MAD_PEAK_T, 4),
@@ -284,7 +292,7 @@ def main():
                      "the host adds); latency_ms = one synchronous (N > 1: sharded) MSM" % PIPE_DEPTH),
         "latency_ms": round(lat_ms, 4),
         "hip_hw_queues": {"value": _process_env("GPU_MAX_HW_QUEUES"),
-                          "set_by": "environment" if hwq_preset else "libgnark_mi355x.so load-time default"},
+                          "set_by": "environment" if hwq_preset else "unset (HIP's default)"},
     }
 
     if rank == 0 and not args.no_secondary and world == 1:
@@ -395,9 +403,18 @@ def secondary(ctx, gm, args):
                 res["groth16"].append(groth16_bench(ctx, gm, l, precompute=False,
                                                     check_oracle=("full" if l <= 20 else
                                                                   "host" if not args.no_cpu_baseline else None),
-                                                    staged=True))
+                                                    staged=True, first_proof=l >= 24))
             if not args.g16_no_precomputed:
                 res["groth16"].append(groth16_bench(ctx, gm, l, precompute=True))
+            # GM_PK_PRECOMPUTE_AUTO's trade: the window copies' extra upload time
+            # against what they save per proof (device inputs)
+            ent = {e["pk"]: e for e in res["groth16"] if e["logn"] == l}
+            if len(ent) == 2:
+                save_ms = ent["plain"]["prove_ms_device_inputs"] - ent["precomputed"]["prove_ms_device_inputs"]
+                extra_s = ent["precomputed"]["pk_upload_s"] - ent["plain"]["pk_upload_s"]
+                ent["precomputed"]["precompute_break_even"] = {
+                    "extra_upload_s": round(extra_s, 3), "saved_ms_per_proof": round(save_ms, 3),
+                    "proofs": round(extra_s * 1e3 / save_ms, 1) if save_ms > 0 else None}
     return res
 
 
@@ -473,7 +490,7 @@ def synthetic_pk(ctx, gm, n, nb_wires, nb_public, slices=None):
     return pk
 
 
-def groth16_bench(ctx, gm, logn, precompute=True, check_oracle=False, staged=False):
+def groth16_bench(ctx, gm, logn, precompute=True, check_oracle=False, staged=False, first_proof=False):
     """Groth16 prove at n = 2^logn (synthetic pk of random points, synthetic
     solution vectors), timed in two scopes:
       host:   wires / a / b / c in host memory, gm_g16_prove -- the scope of
@@ -490,7 +507,11 @@ def groth16_bench(ctx, gm, logn, precompute=True, check_oracle=False, staged=Fal
     nb_wires = n + 2
     nb_public = 2
     pk = synthetic_pk(ctx, gm, n, nb_wires, nb_public)
+    ctx.synchronize()
+    t0 = time.perf_counter()
     dpk = gm.ProvingKey(ctx, "bn254", pk, n, nb_wires, nb_public, precompute=precompute)
+    ctx.synchronize()
+    t_upload = time.perf_counter() - t0  # host arrays -> device layout (+ window copies), computeH tables
     W = ctx.random_scalars("bn254", nb_wires, 8)
     srcs = [ctx.random_scalars("bn254", n, 9 + i) for i in range(3)]
     r = ctx.random_scalars("bn254", 2, 12).to_host()
@@ -500,6 +521,7 @@ def groth16_bench(ctx, gm, logn, precompute=True, check_oracle=False, staged=Fal
     # R1CS's first touch), then `reps` timed ones: median and best reported
     reps = 3
     t_dev, t_host = [], []
+    t_first = None
     for i in range(reps + 1):
         for dst, src in zip((A, B, C), srcs):
             dst.copy_from(src)
@@ -508,6 +530,8 @@ def groth16_bench(ctx, gm, logn, precompute=True, check_oracle=False, staged=Fal
         dpk.prove_device(W, A, B, C, n, r[:32], r[32:])
         if i:
             t_dev.append(time.perf_counter() - t0)
+        else:
+            t_first = time.perf_counter() - t0  # the key's first prove (its workspace grows)
     proof = None
     dpk.prove(host[0], host[1], host[2], host[3], r[:32], r[32:])
     for _ in range(reps):
@@ -526,16 +550,16 @@ def groth16_bench(ctx, gm, logn, precompute=True, check_oracle=False, staged=Fal
         t0 = time.perf_counter()
         proof_r1cs = dpk.prove_r1cs(ch, host[0], r[:32], r[32:])
         t_r1cs.append(time.perf_counter() - t0)
-    # R1CS resident + wires staged during Solve (the wire-extended level hook: 64
-    # pieces put before the timer), then gm_g16_stage_prove_r1cs: nothing crosses
-    # PCIe after Solve
-    t_r1cs_staged, proof_r1cs_staged = [], None
-    nw = nb_wires
+    # R1CS resident + wires staged during Solve in the reference benchmark
+    # circuit's level shape (groth16_test.go:120-156: one solved wire per solver
+    # level, solver.go:471-484), gathered as the Go level hook does (a put every
+    # 65,536 ids, integration/go/icicle_bn254/staged.go; the replay is the
+    # test-only gm_test_stage_replay_chain), then gm_g16_stage_prove_r1cs:
+    # nothing crosses PCIe after Solve
+    t_r1cs_staged, proof_r1cs_staged, ns_level = [], None, []
     for i in range(reps + 1):
         st = dpk.stage(n)
-        wstep = max(1, nw // 64)
-        for lo in range(0, nw, wstep):
-            st.put_range(st.WIRES, lo, host[0][32 * lo:32 * min(nw, lo + wstep)])
+        ns_level.append(st.replay_chain(host[0], 3, n))
         ctx.synchronize()
         time.sleep(0.05)  # the staged copies finish during "Solve"
         t0 = time.perf_counter()
@@ -554,17 +578,23 @@ def groth16_bench(ctx, gm, logn, precompute=True, check_oracle=False, staged=Fal
            "best_ms": {"host_inputs": round(min(t_host) * 1e3, 3), "device_inputs": round(min(t_dev) * 1e3, 3),
                        "r1cs_resident": round(min(t_r1cs) * 1e3, 3),
                        "r1cs_resident_wires_staged": round(min(t_r1cs_staged) * 1e3, 3)},
+           "pk_upload_s": round(t_upload, 3), "first_prove_ms_device_inputs": round(t_first * 1e3, 3),
+           "stage_host_ns_per_level_wires": round(sorted(ns_level)[len(ns_level) // 2], 1),
            "runs": reps, "warmup": 1, "stat": "median",
            "scope": "host_inputs = icicle.go:204-412 incl. H2D of wires/a/b/c; device_inputs = same with inputs "
                     "resident; r1cs_resident = host wires only (a/b/c from the device-resident R1CS, "
                     "gm_g16_prove_r1cs); r1cs_resident_wires_staged = the same with the wires staged during "
-                    "Solve (gm_g16_stage_prove_r1cs, the Go default path with the wire level hook); all after "
-                    "Solve"}
+                    "Solve in one-wire solver levels (gm_g16_stage_prove_r1cs, the Go default path with the "
+                    "wire level hook; stage_host_ns_per_level_wires = the Solve-side cost of that staging); all "
+                    "after Solve; pk_upload_s = host arrays to the device key incl. window copies and computeH "
+                    "tables; first_prove_ms_device_inputs = the key's first prove in this process"}
     if check_oracle or staged:
         res.update(staged_bench(ctx, dpk, n, host, r, proof))
     if check_oracle == "full":
         res.update(io_bench(ctx, gm, dpk, pk, n, nb_wires, nb_public, host, r, proof))
     dpk.free()
+    if first_proof:
+        res["time_to_first_proof"] = first_proof_bench(gm, pk, n, nb_wires, nb_public, host, r, proof)
     for b in [W, A, B, C] + srcs:
         b.free()
     if check_oracle:
@@ -654,46 +684,41 @@ def groth16_roofline(n, nb_wires, precompute, t_s):
 
 
 def staged_bench(ctx, dpk, n, host, r, host_proof):
-    """SURVEY.md §8f row 4 on the same key (gm_g16_stage_*), a / b / c handed over
-    in 64 "solver levels" before the timer starts (the level hook runs them
-    during Solve), then two timed scopes after Solve:
-      wires_after_solve: the wires copied inside the timer, then the prove -- the
-              Go staged path as integration/go/icicle_bn254/staged.go runs it
-              (its prove(): PutRange(StageWires) then Prove);
-      all_during_solve:  the wires also staged during Solve (64 ranges, as the
-              wire-extended level hook hands them over), only the prove timed.
-    The first stage of each scope is an untimed warm-up (the key keeps the stage
-    buffers for the next proof)."""
+    """SURVEY.md §8f row 4 on the same key (gm_g16_stage_*): a / b / c and the
+    wires handed over during "Solve" in the reference benchmark circuit's level
+    shape (groth16_test.go:120-156, a chain of squarings: every solver level
+    finishes one constraint and solves one wire, solver.go:471-484), gathered as
+    the Go level hook does (integration/go/icicle_bn254/staged.go: a put every
+    65,536 ids; replayed by the test-only gm_test_stage_replay_chain), then only
+    the prove timed (gm_g16_stage_prove).  The first stage is an untimed warm-up
+    (the key keeps the stage buffers for the next proof).  The Solve-side cost
+    per level is reported for the gathered puts and, on a 2^20-level sample, for
+    one put per level and vector (no gathering in the hook)."""
     out = {}
     reps = 3
-    proofs = {}
-    for scope in ("wires_after_solve", "all_during_solve"):
-        ts = []
-        for i in range(reps + 1):
-            st = dpk.stage(n)
-            step = max(1, n // 64)
-            for lo in range(0, n, step):
-                for which, v in ((st.A, host[1]), (st.B, host[2]), (st.C, host[3])):
-                    st.put_range(which, lo, v[32 * lo:32 * (lo + step)])
-            nw = len(host[0]) // 32
-            if scope == "all_during_solve":
-                wstep = max(1, nw // 64)
-                for lo in range(0, nw, wstep):
-                    st.put_range(st.WIRES, lo, host[0][32 * lo:32 * min(nw, lo + wstep)])
-            ctx.synchronize()
-            time.sleep(0.05)  # the staged copies finish during "Solve"
-            t0 = time.perf_counter()
-            if scope == "wires_after_solve":
-                st.put_range(st.WIRES, 0, host[0])
-            proof = st.prove(r[:32], r[32:])
-            if i:
-                ts.append(time.perf_counter() - t0)
-            st.free()
-        out["prove_ms_staged_" + scope] = round(sorted(ts)[reps // 2] * 1e3, 3)
-        proofs[scope] = proof
-    out["staged_matches_host_scope"] = bool(all(p == host_proof for p in proofs.values()))
-    out["staged_scope"] = ("a/b/c staged by level before the timer in both; wires_after_solve = staged.go's "
-                           "prove() (wires H2D + prove), all_during_solve = prove only")
+    ts, ns, proof = [], [], None
+    abc = (host[1], host[2], host[3])
+    for i in range(reps + 1):
+        st = dpk.stage(n)
+        ns.append(st.replay_chain(host[0], 3, n, abc=abc))
+        ctx.synchronize()
+        time.sleep(0.05)  # the staged copies finish during "Solve"
+        t0 = time.perf_counter()
+        proof = st.prove(r[:32], r[32:])
+        if i:
+            ts.append(time.perf_counter() - t0)
+        st.free()
+    k = min(n, 1 << 20)
+    st = dpk.stage(n)
+    ns_each = st.replay_chain(host[0], 3, k, abc=abc, coalesce=False)
+    st.free()
+    out["prove_ms_staged_all_during_solve"] = round(sorted(ts)[reps // 2] * 1e3, 3)
+    out["staged_matches_host_scope"] = bool(proof == host_proof)
+    out["stage_host_ns_per_level"] = {"gathered": round(sorted(ns)[len(ns) // 2], 1),
+                                      "one_put_per_level_and_vector": round(ns_each, 1),
+                                      "levels": n, "sample_levels_one_put": k}
+    out["staged_scope"] = ("a/b/c and wires staged during Solve in one-constraint / one-wire levels (gathered "
+                           "puts, as staged.go's hook), prove only timed")
     return out
 
 
@@ -729,6 +754,63 @@ def io_bench(ctx, gm, dpk, pk, n, nb_wires, nb_public, host, r, proof):
                       "cache_save_s": round(t_save, 4), "cache_load_s": round(t_load, 4),
                       "proofs_match": bool(ok),
                       "note": "dump file in the page cache (local tmp); device-layout cache = same point bytes"}
+    return out
+
+
+def first_proof_bench(gm, pk, n, nb_wires, nb_public, host, r, proof):
+    """Time to first proof (the reference uploads the key
+    lazily inside the first Prove, icicle.go:145-150 -> :31-130): the key written
+    as a WriteDump file (marshal.go:389-456), then in a FRESH process each
+    (tools/first_proof.py): library + context, the key streamed from the dump
+    (plain / GM_PK_PRECOMPUTE_AUTO, which picks the window copies on MI355X) or
+    read back from a device-layout cache of the plain key, and the first and a
+    second host-input prove.  Files in the local TMPDIR."""
+    import subprocess
+    import tempfile
+    out = {}
+    meta = {k: pk[k] for k in ("g1_alpha", "g1_beta", "g1_delta", "g2_beta", "g2_delta", "infA", "infB")}
+    meta["counts"] = (nb_wires, nb_wires, nb_wires - nb_public)
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "pk.dump")
+        t0 = time.perf_counter()
+        off = gm.write_dump_slices(path, "bn254", pk, b"\0" * 4096)
+        out["dump_bytes"] = os.path.getsize(path) - off
+        out["dump_write_s"] = round(time.perf_counter() - t0, 2)
+        inp = os.path.join(d, "inputs.npz")
+        np_ = __import__("numpy")
+        np_.savez(inp, **{k: np_.asarray(v) for k, v in meta.items() if k != "counts"},
+                  counts=np_.array(meta["counts"], np_.uint64), domain_size=n, nb_wires=nb_wires,
+                  nb_public=nb_public, W=host[0], a=host[1], b=host[2], c=host[3], r=np_.frombuffer(r, np_.uint8))
+
+        def child(target, mode):
+            t = time.perf_counter()
+            rr = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "first_proof.py"), inp, target, str(off),
+                                 mode], capture_output=True, text=True, timeout=600)
+            if rr.returncode != 0:
+                return {"error": (rr.stderr or rr.stdout)[-300:]}
+            j = json.loads(rr.stdout.strip().splitlines()[-1])
+            j["process_wall_s"] = round(time.perf_counter() - t, 3)
+            j["proof_matches"] = bytes.fromhex(j.pop("proof_hex")) == b"".join(proof)
+            return j
+
+        out["fresh_process_dump_plain"] = child(path, "0")
+        out["fresh_process_dump_auto"] = child(path, "auto")
+        # the device-layout cache of the plain key, written by a key streamed from the dump
+        cpath = os.path.join(d, "pk.cache")
+        import gnark_mi355x as gmm
+        ctx2 = gmm.Context(0)
+        try:
+            k2, _ = gmm.ProvingKey.from_dump(ctx2, "bn254", path, off, meta, n, nb_wires, nb_public)
+            t0 = time.perf_counter()
+            k2.save_cache(cpath)
+            out["cache_save_s"] = round(time.perf_counter() - t0, 2)
+            k2.free()
+        finally:
+            ctx2.close()
+        os.remove(path)
+        out["fresh_process_cache_plain"] = child(cpath, "cache")
+    out["note"] = ("fresh process per line (python + numpy + the library, no torch); to_first_proof_s counts from "
+                   "the interpreter's first statement; dump / cache files in the local TMPDIR (page cache)")
     return out
 
 

@@ -9,25 +9,16 @@
 #include <vector>
 
 #include "curves.hpp"
+#include "groth16.hpp"
 #include "msm.hpp"
 #include "ntt.hpp"
 #include "runtime.hpp"
-
-// Hardware queues: every in-flight MSM (gm_msm_async) runs on a stream of its own,
-// and with HIP's default of 4 hardware queues per process those streams share a
-// queue with the context's main / aux / copy streams and run back to back.  HIP
-// reads GPU_MAX_HW_QUEUES when its runtime initialises (the first HIP call), so
-// the library raises the default to 8 while it is being loaded -- only when the
-// variable is unset, so a process (or gnark's Go host) that chose a value keeps it.
-// Back-to-back 2^20 G1 MSMs: 503-520 -> 530-554 Mpoints/s (profiles/r04m_hwq_ab.txt).
-__attribute__((constructor)) static void gm_default_hw_queues() {
-  if (!getenv("GPU_MAX_HW_QUEUES")) setenv("GPU_MAX_HW_QUEUES", "8", 0);
-}
 
 namespace gm {
 
 static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
+std::string last_error() { return g_last_error; }
 
 // ---------------------------------------------------------------------------
 // synthetic-input kernels (bench / tests)
@@ -149,8 +140,6 @@ int gm_init(int device, gm_ctx** out) {
   GM_HIP(hipSetDevice(device));
   auto* c = new gm_ctx();
   c->device = device;
-  // GM_MSM_SLICE: entries per thread in the bucket accumulation (tuning; default 64)
-  if (const char* sl = getenv("GM_MSM_SLICE")) c->msm_slice = atoi(sl) > 0 ? atoi(sl) : 0;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
@@ -173,6 +162,8 @@ int gm_destroy(gm_ctx* ctx) {
     if (s) hipStreamSynchronize(s);
   if (ctx->g16_stream) hipStreamSynchronize(ctx->g16_stream);
   orphan_pending_msms(ctx);
+  // stages parked with keys of this context (their keys may outlive it)
+  while (!ctx->spare_keys.empty()) stage_spare_release(ctx->spare_keys.back());
   for (auto& pr : ctx->pending_reads) hipEventDestroy(pr.second);
   ctx->pending_reads.clear();
   ntt_domains_free(ctx);
@@ -192,6 +183,7 @@ int gm_destroy(gm_ctx* ctx) {
   for (hipStream_t s : ctx->slot_stream)
     if (s) hipStreamDestroy(s);
   if (ctx->g16_stream) hipStreamDestroy(ctx->g16_stream);
+  if (ctx->acc_tail) hipEventDestroy(ctx->acc_tail);
   hipStreamDestroy(ctx->stream);
   if (ctx->aux) hipStreamDestroy(ctx->aux);
   if (ctx->copy) hipStreamDestroy(ctx->copy);
@@ -229,6 +221,7 @@ int gm_trim(gm_ctx* ctx) {
   if (ctx->in_abc) hipFree(ctx->in_abc);
   ctx->in_abc = nullptr;
   ctx->in_abc_cap = 0;
+  while (!ctx->spare_keys.empty()) stage_spare_release(ctx->spare_keys.back());  // parked stages
   for (int i = 0; i < gm_ctx::H2D_SLOTS; i++) {
     if (ctx->h2d_pin[i]) hipHostFree(ctx->h2d_pin[i]);
     ctx->h2d_pin[i] = nullptr;
@@ -374,10 +367,9 @@ bool gm::msm_glv_on(const gm_ctx* ctx, bool g2, size_t n) {
   // 2^20 it halves the bucket reduction (BN254 G1 2.26 -> 2.14 ms, G2 7.65 ->
   // 6.51 ms); at 2^22 (BLS12-377) the reduction is a small share while the 2n
   // virtual points double the gathered point set (G1 14.2 -> 15.8 ms, G2 56.6
-  // -> 62.1 ms).  GM_MSM_GLV_MAXLOG overrides the bound.
-  static const int maxlog = getenv("GM_MSM_GLV_MAXLOG") ? atoi(getenv("GM_MSM_GLV_MAXLOG")) : 21;
-  if (n > (size_t(1) << std::max(0, std::min(40, maxlog)))) return false;
-  return msm_glv_enabled() && (!g2 || msm_glv_g2_enabled());
+  // -> 62.1 ms).  gm_set_msm_glv overrides it per context.
+  if (n > (size_t(1) << 21)) return false;
+  return true;
 }
 
 // MsmTail's pinned readback buffer goes back to its context (msm.hpp)
@@ -438,32 +430,23 @@ int gm_msm_async(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const 
   p->curve = curve;
   p->g2 = g2 ? 1 : 0;
   int rc = p->slot.take();
-  // One stream per slot (GM_MSM_SLOT_STREAMS=0: everything on ctx->stream).  With
-  // a hardware queue per stream (GPU_MAX_HW_QUEUES >= 8: HIP's default 4 puts both
-  // slot streams on one queue) one MSM's fixup / reduction / readback overlaps the
-  // next one's accumulation: back-to-back 2^20 G1 MSMs 1.95-1.99 -> 1.90-1.92 ms
-  // (profiles/r04m_hwq_ab.txt).  It starts after the work already queued on
-  // ctx->stream (the inputs).
-  static const bool slot_streams = !getenv("GM_MSM_SLOT_STREAMS") || atoi(getenv("GM_MSM_SLOT_STREAMS")) != 0;
+  // One stream per slot: one MSM's fixup / reduction / readback overlaps the
+  // next one's conversion and sort (profiles/r04m_hwq_ab.txt, r05r_slot_stream_ab.txt).
+  // It starts after the work already queued on ctx->stream (the inputs).
   hipEvent_t inputs_read = nullptr;
   p->st = ctx->stream;
-  if (rc == GM_OK && slot_streams) {
+  if (rc == GM_OK) {
     hipStream_t& ss = ctx->slot_stream[p->slot.k];
     // The slot streams run at the highest stream priority: the runtime keeps a
     // separate pool of hardware queues per priority, so with the default four
     // queues they do not share one with ctx->stream / aux / copy or each other,
     // and the next MSM's conversion and sort start beside this one's reduction
     // (bench 2^20: 599-605 -> 632-645 Mpoints/s with the change below,
-    // profiles/r05r_slot_stream_ab.txt).  GM_MSM_SLOT_PRIO=0: normal priority.
-    static const bool prio = !getenv("GM_MSM_SLOT_PRIO") || atoi(getenv("GM_MSM_SLOT_PRIO")) != 0;
+    // profiles/r05r_slot_stream_ab.txt).
     if (!ss) {
-      if (prio) {
-        int least = 0, greatest = 0;
-        GM_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        GM_HIP(hipStreamCreateWithPriority(&ss, hipStreamNonBlocking, greatest));
-      } else {
-        GM_HIP(hipStreamCreateWithFlags(&ss, hipStreamNonBlocking));
-      }
+      int least = 0, greatest = 0;
+      GM_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+      GM_HIP(hipStreamCreateWithPriority(&ss, hipStreamNonBlocking, greatest));
     }
     // Ordered after the work already queued on ctx->stream (the inputs) -- by a
     // marker only when that stream still has work: a packet on ctx->stream waits
@@ -485,7 +468,13 @@ int gm_msm_async(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const 
     GM_HIP(hipEventCreateWithFlags(&inputs_read, hipEventDisableTiming));
   }
   {
+    static const bool acc_serial = getenv("GM_MSM_ACC_SERIAL") && atoi(getenv("GM_MSM_ACC_SERIAL")) != 0;
+    ctx->acc_chain = acc_serial && p->st != ctx->stream;  // slot streams only
     StreamSwap sw(ctx, p->st);
+    struct ChainOff {
+      gm_ctx* c;
+      ~ChainOff() { c->acc_chain = false; }
+    } chain_off{ctx};
     if (rc == GM_OK) {
       Arena& a = *p->slot.a;
       const void* sc = scalars_dev;

@@ -252,6 +252,8 @@ int pk_upload_ranges(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsigned f
     // the streamed (dump) path builds a shared array's compacted precomputed copy
     // before expanding it: one more array at the upload's peak
     if (src && (pk->wshare[0] || pk->wshare[1] || pk->wshare[2])) need += largest;
+    // computeH's two n-element tables, built at the end of the upload (pk_prepare_h)
+    need += 2.0 * 36.0 * (double)pk->n;
     size_t fr = 0, tot = 0;
     const char* fenv = getenv("GM_PK_PRECOMPUTE_FRAC");
     const double frac = fenv ? atof(fenv) : 0.6;
@@ -406,11 +408,13 @@ int pk_upload_ranges(gm_ctx* ctx, int curve, const gm_g16_pk_host* h, unsigned f
 }
 
 void pk_prepare_h(gm_ctx* ctx, const gm_g16_pk* pk) {
-  static const bool on = !getenv("GM_G16_PREPARE_H") || atoi(getenv("GM_G16_PREPARE_H")) != 0;
-  if (!on) return;
+  const std::string saved = last_error();
   const int rc = pk->curve == GM_BN254 ? compute_h_prepare<CurveBN254>(ctx, pk->n)
                                        : compute_h_prepare<CurveBLS12377>(ctx, pk->n);
-  if (rc) (void)hipGetLastError();  // e.g. out of memory: the first prove builds them (or reports it)
+  if (rc) {  // e.g. out of memory: the first prove builds them (or reports it); the upload succeeded
+    (void)hipGetLastError();
+    set_error(saved);
+  }
 }
 
 namespace {
@@ -429,26 +433,17 @@ struct HSource {
 
 // computeH on the context's auxiliary stream, overlapped with the MSMs (whose
 // sorts, reductions and host round trips leave the VALUs idle).
-// GM_G16_OVERLAP=0 runs it in order on the main stream (A/B measurements).
 // r1: a, b, c are first evaluated from the wires by the device-resident R1CS
 // (gm_g16_prove_r1cs), on the same stream as computeH.
 template <class C>
 int launch_compute_h(gm_ctx* ctx, void* a, void* b, void* c, size_t nc, size_t n, hipEvent_t wait_for,
                      hipEvent_t done, const gm_r1cs* r1 = nullptr, const void* wires = nullptr) {
-  static const bool overlap = !getenv("GM_G16_OVERLAP") || atoi(getenv("GM_G16_OVERLAP")) != 0;
   // n == 0: only the R1CS evaluation (no done event); computeH follows later
   auto body = [&]() -> int {
     int rc;
     if (r1 && (rc = r1cs_eval_device(ctx, r1, wires, a, b, c))) return rc;
     return n ? compute_h_device<C>(ctx, a, b, c, nc, n) : GM_OK;
   };
-  if (!overlap) {
-    if (wait_for) GM_HIP(hipStreamWaitEvent(ctx->stream, wait_for, 0));
-    int rc = body();
-    if (rc) return rc;
-    if (done) GM_HIP(hipEventRecord(done, ctx->stream));
-    return GM_OK;
-  }
   if (wait_for) GM_HIP(hipStreamWaitEvent(ctx->aux, wait_for, 0));
   hipStream_t main = ctx->stream;
   ctx->stream = ctx->aux;
@@ -489,15 +484,13 @@ struct DeviceH : HSource {
   // it: the LDS-heavy sort passes and NTT passes slow each other down (r03
   // timeline: k_msm_s2_local 1.2 -> 14.5 ms beside the NTT) while the
   // VALU-bound accumulation shares the chip with them at no extra cost.
-  // GM_G16_H_AFTER_PLAN=0 queues it at once (A/B).  The R1CS evaluation (a
+  // The R1CS evaluation (a
   // latency-bound gather, 0.65 ms alone at 2^24 but 18 ms beside the
   // accumulation) is not deferred: it runs on the auxiliary stream next to the
   // digit pass.
   int start() {
     int rc;
     if ((rc = ev.create())) return rc;
-    static const bool after_plan = !getenv("GM_G16_H_AFTER_PLAN") || atoi(getenv("GM_G16_H_AFTER_PLAN")) != 0;
-    if (!after_plan) return launch();
     if (r1) {
       GM_HIP(hipEventRecord(ev.a, ctx->stream));
       if ((rc = launch_compute_h<C>(ctx, a, b, c, nc, 0, ev.a, nullptr, r1, wires))) return rc;
@@ -588,16 +581,15 @@ struct HostStagedH : HSource {
     int rc;
     if ((rc = ev.create())) return rc;
     for (hipEvent_t& e : vev) GM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    // GM_G16_H2D_PINNED=0: plain pageable copies (A/B).  A pageable copy issued
+    // A pageable copy issued
     // from this thread while the MSMs ran could stall until an accumulation kernel
     // ended (fresh process: copies after the B2 MSM, 2^24 prove 199 ms instead of
     // ~167, profiles/r04s_g16_host_slow_copies.txt); through the context's pinned
     // ring (memcpy into a 32 MiB slot, then an async copy from pinned memory) the
     // DMA does not wait for the kernels.  The slot fill is split over
-    // GM_G16_H2D_THREADS (4) threads: with one, a 32 MiB fill took 1.55 ms against
+    // H2D_FILL_THREADS (4) threads: with one, a 32 MiB fill took 1.55 ms against
     // the DMA's 0.59 ms and a, b, c arrived only ~75 ms into a 2^24 prove
     // (profiles/r05i_host_prove_timeline.txt).
-    static const bool pinned = !getenv("GM_G16_H2D_PINNED") || atoi(getenv("GM_G16_H2D_PINNED")) != 0;
     th = std::thread([this] {
       int r = GM_OK;
       if (hipSetDevice(ctx->device) != hipSuccess) r = GM_ERR_DEVICE;
@@ -605,7 +597,7 @@ struct HostStagedH : HSource {
       void* dst[3] = {da, db, dc};
       // the ring is created on first use; when pinned memory (or an event) is not
       // available the copies take the pageable path instead of failing the prove
-      const bool ring = pinned && r == GM_OK && h2d_ring_ensure(ctx);
+      const bool ring = r == GM_OK && h2d_ring_ensure(ctx);
       bool used[gm_ctx::H2D_SLOTS] = {};
       int slot = 0;
       for (int k = 0; k < 3 && r == GM_OK; k++) {
@@ -614,7 +606,7 @@ struct HostStagedH : HSource {
             const size_t len = std::min(gm_ctx::H2D_SLOT, 32 * nc - off);
             if (used[slot] && hipEventSynchronize(ctx->h2d_ev[slot]) != hipSuccess) r = GM_ERR_DEVICE;
             if (r) break;
-            par_memcpy(ctx->h2d_pin[slot], (const char*)src[k] + off, len, h2d_fill_threads());
+            par_memcpy(ctx->h2d_pin[slot], (const char*)src[k] + off, len, H2D_FILL_THREADS);
             if (hipMemcpyAsync((char*)dst[k] + off, ctx->h2d_pin[slot], len, hipMemcpyHostToDevice, ctx->copy) !=
                     hipSuccess ||
                 hipEventRecord(ctx->h2d_ev[slot], ctx->copy) != hipSuccess)
@@ -635,8 +627,7 @@ struct HostStagedH : HSource {
   }
   // computeH in pieces as the inputs arrive: the chain of vector k (pad, INTT,
   // coset NTT) waits only for k's copies, the fused tail for all three
-  // (launch_compute_h's stream choice: ctx->aux, or the main stream with
-  // GM_G16_OVERLAP=0).  block: wait for every copy to be queued.
+  // (on ctx->aux, as launch_compute_h).  block: wait for every copy to be queued.
   int launch(bool block) {
     if (launched) return GM_OK;
     if (block && th.joinable()) th.join();
@@ -645,13 +636,9 @@ struct HostStagedH : HSource {
       set_error(copy_err);
       return copy_rc;
     }
-    // GM_G16_H_INCREMENTAL=0: no chain before all three vectors are queued (A/B)
-    static const bool incremental = !getenv("GM_G16_H_INCREMENTAL") || atoi(getenv("GM_G16_H_INCREMENTAL")) != 0;
-    int q = nq.load();
-    if (!incremental && q < 3) q = 0;
+    const int q = nq.load();
     if (chained >= q && !(block && q == 3)) return GM_OK;
-    static const bool overlap = !getenv("GM_G16_OVERLAP") || atoi(getenv("GM_G16_OVERLAP")) != 0;
-    const hipStream_t hst = overlap ? ctx->aux : ctx->stream;
+    const hipStream_t hst = ctx->aux;
     void* vec[3] = {da, db, dc};
     {
       StreamSwap sw(ctx, hst);
@@ -1457,14 +1444,12 @@ int gm_g16_pk_upload_multi(gm_multi* m, int curve, const gm_g16_pk_host* h, unsi
   // the MSM work (GM_MULTI_SHARE0 = its weight relative to the others' 1.0)
   // devices 0-2 also run computeH (split: one a / b / c chain each, device 0
   // the tail and the h distribution; ~5 ms per chain, ~2.5 ms tail at 2^24):
-  // they take smaller MSM shares (GM_MULTI_SHARE0 / GM_MULTI_SHARE_H = weight
-  // relative to the others' 1.0)
+  // they take smaller MSM shares (weights relative to the others' 1.0; an
+  // estimate from the one-GPU timeline)
   std::vector<double> w(nd, 1.0);
   if (nd > 1) {
-    const char* s0 = getenv("GM_MULTI_SHARE0");
-    const char* sh = getenv("GM_MULTI_SHARE_H");
-    w[0] = s0 ? std::max(0.0, atof(s0)) : 0.7;
-    for (int d = 1; d < std::min(nd, 3); d++) w[d] = sh ? std::max(0.0, atof(sh)) : 0.85;
+    w[0] = 0.7;
+    for (int d = 1; d < std::min(nd, 3); d++) w[d] = 0.85;
   }
   auto* mp = new gm_g16_pk_multi();
   mp->curve = curve;

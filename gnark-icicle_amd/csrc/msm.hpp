@@ -89,19 +89,8 @@ struct MsmPlan {
 template <class C>
 int msm_plan(gm_ctx* ctx, Arena& arena, const void* scalars_dev, size_t n, const MsmPrecomp* pre,
              MsmPlan& plan, bool glv = false);
-// GLV used for plain MSMs from gnark-layout points (GM_MSM_GLV=0 disables)
-inline bool msm_glv_enabled() {
-  static const bool on = !(getenv("GM_MSM_GLV") && getenv("GM_MSM_GLV")[0] == '0');
-  return on;
-}
-// ... and for G2 (phi(x, y) = (beta^2 x, y) on the twist; GM_MSM_GLV_G2=0 disables)
-inline bool msm_glv_g2_enabled() {
-  static const bool on = !(getenv("GM_MSM_GLV_G2") && getenv("GM_MSM_GLV_G2")[0] == '0');
-  return on;
-}
 // GLV for an MSM of n points on ctx: the context's setting (gm_set_msm_glv)
-// or, by default, the environment's (GM_MSM_GLV / GM_MSM_GLV_G2) for n up to
-// 2^21 (GM_MSM_GLV_MAXLOG)
+// or, by default, on for n up to 2^21 (G1 and G2)
 bool msm_glv_on(const gm_ctx* ctx, bool g2, size_t n);
 template <class C, bool G2>
 int msm_run(gm_ctx* ctx, const MsmPlan& plan, const void* points_internal,

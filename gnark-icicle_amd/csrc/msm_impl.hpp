@@ -352,21 +352,8 @@ __global__ void __launch_bounds__(1024) k_msm_digits_glv(const uint32_t* __restr
     if (dg_lds[q]) atomicAdd(&ccount[q], dg_lds[q]);
 }
 
-// gnark-layout points -> internal layout, plus phi(P_i) = (beta x, y) at n + i
-// (the GLV point set; G2: beta^2 on the twist)
-template <class F>
-__global__ void __launch_bounds__(256) k_msm_convert_points_glv(const uint32_t* __restrict__ src, size_t n,
-                                                                uint32_t* __restrict__ dst) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  constexpr int PW = 2 * Coord<F>::WORDS;
-  Affine<F> a = load_affine_gnark<F>(src + i * PW);
-  store_affine_packed<F>(dst + i * PW, a);
-  a.x = glv_phi_x(a.x);
-  store_affine_packed<F>(dst + (n + i) * PW, a);
-}
-
-// The same conversion with coalesced HBM traffic: a block stages its 256 points
+// gnark-layout points -> internal layout (GLV: plus phi(P_i) = (beta x, y) at
+// n + i; G2: beta^2 on the twist), with coalesced HBM traffic: a block stages its 256 points
 // through LDS (16-B lane loads / stores over contiguous bytes) and converts
 // from there, instead of each lane reading and writing 64 B at a 64-B lane
 // stride.  GLV: the phi copy goes out through the same LDS tile.  LDS rows are
@@ -527,93 +514,8 @@ GM_DEV void accum_emit(uint32_t b, const XYZZ<F>& acc_raw, bool is_first, bool i
   }
 }
 
-// PREFETCH: the next entry's point words are loaded while this add runs.
-// IDXPF (without PREFETCH): only the next entry's key and value are, so the
-// point address of each iteration is known when it starts.
-template <class F, bool PREFETCH, bool IDXPF = false, bool CH = false>
-GM_DEV void accum_seg_body(const uint32_t* __restrict__ points, uint32_t n,
-                                                       const uint32_t* __restrict__ keys,
-                                                       const uint32_t* __restrict__ vals,
-                                                       const uint32_t* __restrict__ offsets, uint32_t total,
-                                                       uint32_t K, XYZZ<F>* __restrict__ buckets,
-                                                       XYZZ<F>* __restrict__ part_first,
-                                                       XYZZ<F>* __restrict__ part_last,
-                                                       uint32_t* __restrict__ err) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t Mv = offsets[total];  // valid (non-zero-digit) entries
-  const uint32_t start = t * K;
-  if (start >= Mv) return;
-  const uint32_t end = min(start + K, Mv);
-  uint32_t v = vals[start];
-  uint32_t cur = keys[start];
-  bool first = true;
-  XYZZ<F> acc = xyzz_inf<F>();
-  uint32_t idx = v & 0x7fffffffu;
-  if (idx >= n) {
-    atomicOr(err, 2u);
-    return;
-  }
-  constexpr int PW = 2 * Coord<F>::WORDS;  // u32 words per packed point
-  PackedPt<PW> P = load_packed_pt<PW>(points + (size_t)idx * PW);
-  uint32_t kq = keys[start];
-  for (uint32_t q = start; q < end; q++) {
-    const uint32_t k = IDXPF ? kq : keys[q];
-    uint32_t vi = 0;
-    if (IDXPF && !PREFETCH && q + 1 < end) {
-      kq = keys[q + 1];
-      vi = vals[q + 1];
-    }
-    // prefetch the next point's words while this add runs
-    uint32_t vn = 0;
-    PackedPt<PW> Pn;
-    if (PREFETCH && q + 1 < end) {
-      vn = vals[q + 1];
-      const uint32_t in = vn & 0x7fffffffu;
-      if (in >= n) {
-        atomicOr(err, 2u);
-        return;
-      }
-      Pn = load_packed_pt<PW>(points + (size_t)in * PW);
-    }
-    if (k != cur) {
-      accum_emit(cur, acc, first, false, start, end, t, offsets, buckets, part_first, part_last);
-      first = false;
-      acc = xyzz_inf<F>();
-      cur = k;
-    }
-    if (!PREFETCH) P = load_packed_pt<PW>(points + (size_t)(v & 0x7fffffffu) * PW);
-    Affine<F> A = load_affine_packed<F>(P.w);
-    LazyAcc<F>::template add<CH>(acc, A, (v >> 31) != 0);
-    if (PREFETCH) {
-      v = vn;
-      P = Pn;
-    } else if (q + 1 < end) {
-      v = IDXPF ? vi : vals[q + 1];
-      if ((v & 0x7fffffffu) >= n) {
-        atomicOr(err, 2u);
-        return;
-      }
-    }
-  }
-  accum_emit(cur, acc, first, true, start, end, t, offsets, buckets, part_first, part_last);
-}
-
-
-// G1 default: four waves per SIMD (<= 128 VGPRs, no spill) and no prefetch --
-// the other waves hide the point loads and the mad-chain latency.  Same-box A/B
-// at 2^20 (profiles/r03e_ab.txt): 1.335 ms vs 1.343-1.358 ms for the 3-wave
-// prefetching kernel (k_msm_accum_seg_pf, GM_MSM_ACCUM=prefetch), 1.53 ms with
-// prefetch at four waves (36 VGPRs spilled); precomputed keys 1.41-1.46 vs 1.47.
-template <class F>
-__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4)))
-k_msm_accum_seg(const uint32_t* __restrict__ points, uint32_t n, const uint32_t* __restrict__ keys,
-                const uint32_t* __restrict__ vals, const uint32_t* __restrict__ offsets, uint32_t total,
-                uint32_t K, XYZZ<F>* __restrict__ buckets, XYZZ<F>* __restrict__ part_first,
-                XYZZ<F>* __restrict__ part_last, uint32_t* __restrict__ err) {
-  accum_seg_body<F, false>(points, n, keys, vals, offsets, total, K, buckets, part_first, part_last, err);
-}
-// The default G1 body (k_msm_accum_seg_ch): keys and values arrive four entries
-// per 16-byte load instead of one 4-byte load per entry.  A thread's slice is K
+// G1 accumulation body: keys and values arrive four entries per 16-byte load
+// instead of one 4-byte load per entry (r05).  A thread's slice is K
 // consecutive entries and consecutive lanes are K entries apart, so each 4-byte
 // load touched one cache line per lane and the line rarely survived in L1 until
 // the lane's next entry (rocprofv3 FETCH_SIZE of the accumulation: 2.8 GB per
@@ -684,9 +586,11 @@ GM_DEV void accum_seg_body_v4(const uint32_t* __restrict__ points, uint32_t n, c
   accum_emit(cur, acc, first, true, start, end, t, offsets, buckets, part_first, part_last);
 }
 
-// Same with one dependent mad chain per product inside the add (the default for
-// BN254 G1 since r05; GM_MSM_ACC_CHAIN=0 selects k_msm_accum_seg).  Applied to
-// every MSM kernel it slowed the one-to-two-wave reduction kernels (r04h).
+// BN254 G1: one strict mad chain per product inside the add (r05; the split-
+// column schedule measured slower, profiles/r05e_acc_chain_ab.txt,
+// r05an_strict_chain_ab.txt), four waves per SIMD, no prefetch: the other waves
+// hide the point loads (profiles/r03e_ab.txt).  Applied to every MSM kernel the
+// chains slowed the one-to-two-wave reduction kernels (r04h, r05ax).
 template <class F>
 __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4)))
 k_msm_accum_seg_ch(const uint32_t* __restrict__ points, uint32_t n, const uint32_t* __restrict__ keys,
@@ -695,27 +599,8 @@ k_msm_accum_seg_ch(const uint32_t* __restrict__ points, uint32_t n, const uint32
                    XYZZ<F>* __restrict__ part_last, uint32_t* __restrict__ err) {
   accum_seg_body_v4<F, true>(points, n, keys, vals, offsets, total, K, buckets, part_first, part_last, err);
 }
-// the chain kernel with one 4-byte key / value load per entry (GM_MSM_ACC_V4=0; A/B)
-template <class F>
-__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4)))
-k_msm_accum_seg_ch1(const uint32_t* __restrict__ points, uint32_t n, const uint32_t* __restrict__ keys,
-                    const uint32_t* __restrict__ vals, const uint32_t* __restrict__ offsets, uint32_t total,
-                    uint32_t K, XYZZ<F>* __restrict__ buckets, XYZZ<F>* __restrict__ part_first,
-                    XYZZ<F>* __restrict__ part_last, uint32_t* __restrict__ err) {
-  accum_seg_body<F, false, false, true>(points, n, keys, vals, offsets, total, K, buckets, part_first, part_last,
-                                        err);
-}
-// Same with the next key / value prefetched (GM_MSM_ACCUM=idx; A-B).
-template <class F>
-__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4)))
-k_msm_accum_seg_idx(const uint32_t* __restrict__ points, uint32_t n, const uint32_t* __restrict__ keys,
-                    const uint32_t* __restrict__ vals, const uint32_t* __restrict__ offsets, uint32_t total,
-                    uint32_t K, XYZZ<F>* __restrict__ buckets, XYZZ<F>* __restrict__ part_first,
-                    XYZZ<F>* __restrict__ part_last, uint32_t* __restrict__ err) {
-  accum_seg_body<F, false, true>(points, n, keys, vals, offsets, total, K, buckets, part_first, part_last, err);
-}
 // Four waves fit the 9-limb fields only: BLS12-377's 14-limb add spills 216
-// VGPRs under the cap and keeps the prefetching kernel (2 waves, no spill).
+// VGPRs under the cap and takes the prefetching kernel (two waves, no spill).
 template <class F>
 struct AccumW4 {
   static constexpr bool ok = false;
@@ -724,10 +609,8 @@ template <class P>
 struct AccumW4<Fe<P>> {
   static constexpr bool ok = P::N <= 9;
 };
-// The next point prefetched into registers while the current add runs (three
-// waves per SIMD for BN254 G1, two for BLS12-377 G1).
-// The prefetching kernel with keys / values in groups of four (default for the
-// prefetching kernel when K % 4 == 0; GM_MSM_ACC_V4=0: k_msm_accum_seg_pf).
+// The next point prefetched into registers while the current add runs
+// (BLS12-377 G1: two waves per SIMD).
 template <class F>
 __global__ void __launch_bounds__(128) k_msm_accum_seg_pf4(const uint32_t* __restrict__ points, uint32_t n,
                                                            const uint32_t* __restrict__ keys,
@@ -739,31 +622,15 @@ __global__ void __launch_bounds__(128) k_msm_accum_seg_pf4(const uint32_t* __res
                                                            uint32_t* __restrict__ err) {
   accum_seg_body_v4<F, false, true>(points, n, keys, vals, offsets, total, K, buckets, part_first, part_last, err);
 }
+// G1 accumulation kernel of a field
 template <class F>
-__global__ void __launch_bounds__(128) k_msm_accum_seg_pf(const uint32_t* __restrict__ points, uint32_t n,
-                                                          const uint32_t* __restrict__ keys,
-                                                          const uint32_t* __restrict__ vals,
-                                                          const uint32_t* __restrict__ offsets, uint32_t total,
-                                                          uint32_t K, XYZZ<F>* __restrict__ buckets,
-                                                          XYZZ<F>* __restrict__ part_first,
-                                                          XYZZ<F>* __restrict__ part_last,
-                                                          uint32_t* __restrict__ err) {
-  accum_seg_body<F, true>(points, n, keys, vals, offsets, total, K, buckets, part_first, part_last, err);
+constexpr auto g1_accum_kernel() {
+  if constexpr (AccumW4<F>::ok) return k_msm_accum_seg_ch<F>;
+  else return k_msm_accum_seg_pf4<F>;
 }
 
-// G2 (Fp2 coordinates): a mixed add keeps ~330 registers live, i.e. one wave per
-// SIMD; without the prefetch and with the register budget capped at two waves
-// per SIMD the loads are hidden by the second wave instead.
-template <class F>
-__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2)))
-k_msm_accum_seg_g2(const uint32_t* __restrict__ points, uint32_t n, const uint32_t* __restrict__ keys,
-                   const uint32_t* __restrict__ vals, const uint32_t* __restrict__ offsets, uint32_t total,
-                   uint32_t K, XYZZ<F>* __restrict__ buckets, XYZZ<F>* __restrict__ part_first,
-                   XYZZ<F>* __restrict__ part_last, uint32_t* __restrict__ err) {
-  accum_seg_body<F, false>(points, n, keys, vals, offsets, total, K, buckets, part_first, part_last, err);
-}
-
-// G2 default: Fp2 components split across lane pairs (pair_fp2.hpp).
+// G2: Fp2 components split across lane pairs (pair_fp2.hpp), keys / values in
+// groups of four as in the G1 accumulation.
 template <class F>
 struct PairSel {
   static constexpr bool ok = false;
@@ -771,33 +638,16 @@ struct PairSel {
 template <class P, int B>
 struct PairSel<Fe2<P, B>> {
   static constexpr bool ok = true;
-  // Point prefetch: on for BN254; off for BLS12-377, whose pair kernel spills
-  // at three waves per SIMD (171 -> 135 VGPRs without the prefetch registers;
-  // 2^22 accumulation 46.1 -> 44.2 ms, profiles/r03i_ab.txt).  GM_MSM_PAIR_PF=0/1
-  // overrides.
-  // GM_MSM_PAIR_WPE=3 (A/B): BN254 without prefetch capped at three waves.
-  // keys / values in groups of four (V4, as the G1 accumulation; needs K % 4 == 0):
-  // default on, GM_MSM_ACC_V4=0 off.
-  static auto kernel(uint32_t K) {
-    static const char* pf = getenv("GM_MSM_PAIR_PF");
-    static const char* wpe = getenv("GM_MSM_PAIR_WPE");
-    static const bool v4env = !getenv("GM_MSM_ACC_V4") || atoi(getenv("GM_MSM_ACC_V4")) != 0;
-    const bool v4 = v4env && (K & 3) == 0;
-    // BN254 default since r05: one mad chain per product (fe_mul CHAIN) in the pair
-    // add, no prefetch, three waves per SIMD (168 VGPRs, no spill; the prefetching
-    // kernel needs 200 and runs two): G2 2^20 accumulation 3.91-3.92 -> 3.86-3.89 ms,
-    // Groth16 2^24 148.0-149.3 -> 146.8-147.8 ms (profiles/r05aj_pair_chain_ab.txt).
-    // GM_MSM_PAIR_CHAIN=0 (or GM_MSM_PAIR_PF set): the kernels below.
-    static const bool pch = !getenv("GM_MSM_PAIR_CHAIN") || atoi(getenv("GM_MSM_PAIR_CHAIN")) != 0;
-    if constexpr (P::N <= 9) {
-      if (wpe && wpe[0] == '3') return k_msm_accum_seg_pair<P, B, false, 3>;
-      if (v4 && pch && !pf) return k_msm_accum_seg_pair<P, B, false, 3, true, true>;
-    }
-    const bool on = pf ? pf[0] != '0' : P::N <= 9;
-    if (v4)
-      return on ? k_msm_accum_seg_pair<P, B, true, GM_PAIR_WPE, true>
-                : k_msm_accum_seg_pair<P, B, false, GM_PAIR_WPE, true>;
-    return on ? k_msm_accum_seg_pair<P, B, true> : k_msm_accum_seg_pair<P, B, false>;
+  // BN254: one mad chain per product in the pair add, no prefetch, three waves
+  // per SIMD (168 VGPRs, no spill; the prefetching kernel needs 200 and runs
+  // two): G2 2^20 accumulation 3.91-3.92 -> 3.86-3.89 ms, Groth16 2^24
+  // 148.0-149.3 -> 146.8-147.8 ms (profiles/r05aj_pair_chain_ab.txt).
+  // BLS12-377: no prefetch (its pair kernel spills at three waves with the
+  // prefetch registers: 2^22 accumulation 46.1 -> 44.2 ms, profiles/r03i_ab.txt),
+  // two waves (r04e_g2_ab.txt).
+  static constexpr auto kernel() {
+    if constexpr (P::N <= 9) return k_msm_accum_seg_pair<P, B, false, 3, true, true>;
+    else return k_msm_accum_seg_pair<P, B, false, GM_PAIR_WPE, true>;
   }
   static constexpr auto fixup() { return k_msm_fixup_pair<P, B>; }
   static constexpr auto fix_tree() { return k_msm_fix_tree_pair<P, B>; }
@@ -805,23 +655,9 @@ struct PairSel<Fe2<P, B>> {
   static constexpr auto seg() { return k_msm_seg_pair<P, B>; }
   static constexpr auto bitsum() { return k_msm_bitsum_pair<P, B>; }
 };
-// G2 runs on lane pairs.  The one-lane G2 kernels (a whole Fp2 point per lane;
-// they spill, and the BLS12-377 ones take minutes to compile) are built only
-// with -DGM_G2_ONE_LANE=1, and then GM_MSM_ACCUM=prefetch|noprefetch selects
-// them (A/B).
-#ifndef GM_G2_ONE_LANE
-#define GM_G2_ONE_LANE 0
-#endif
-inline bool g2_pairs() {
-  if (!GM_G2_ONE_LANE) return true;
-  static const char* ov = getenv("GM_MSM_ACCUM");
-  static const bool on = !(ov && (!strcmp(ov, "prefetch") || !strcmp(ov, "noprefetch")));
-  return on;
-}
-// one-lane kernels instantiated for this field: always for G1, for G2 only
-// with GM_G2_ONE_LANE
+// one-lane kernels are instantiated for G1 fields; G2 runs on lane pairs
 template <class F>
-constexpr bool kOneLane = !PairSel<F>::ok || GM_G2_ONE_LANE;
+constexpr bool kOneLane = !PairSel<F>::ok;
 
 // Full adds of the fixup / reduction kernels: lazily reduced for G1
 // (xyzz_add_lz, canonical on store), canonical xyzz_add otherwise.
@@ -1108,11 +944,9 @@ int msm_plan(gm_ctx* ctx, Arena& arena, const void* scalars_dev, size_t n, const
   g.shared_stride = shared ? (uint32_t)pre->stride : 0u;
   g.wn = shared ? W - pre->narrow : W;
   if (!shared && !glv) {
-    // plain layout: balance the windows (see DigitGeom); GM_MSM_PLAIN_NARROW=0 keeps
-    // W full windows and a narrow top one (A/B)
-    static const bool narrow_on = !getenv("GM_MSM_PLAIN_NARROW") || atoi(getenv("GM_MSM_PLAIN_NARROW")) != 0;
+    // plain layout: balance the windows (see DigitGeom)
     const uint32_t narrow = c * W - (uint32_t)(plan.bits + 1);
-    if (narrow_on && narrow < W) g.wn = W - narrow;
+    if (narrow < W) g.wn = W - narrow;
   }
   plan.wn = g.wn;
   g.F = sg.F + sg.G;  // the digits kernel counts pass-1 bins
@@ -1152,8 +986,7 @@ int msm_reduce(gm_ctx* ctx, MsmTail& t) {
   hipStream_t st = ctx->stream;
   ProfScope ps(ctx, "msm_bucket_reduce");
   uint32_t Q = 2;  // points per node: [G, U, Y_0..Y_{Q-3}]
-  bool pairs = false;
-  if constexpr (PairSel<DF>::ok) pairs = g2_pairs();
+  constexpr bool pairs = PairSel<DF>::ok;
   if constexpr (PairSel<DF>::ok) {
     if (pairs)
       hipLaunchKernelGGL(PairSel<DF>::seg(), dim3(blocks_for(2 * (size_t)t.Wr * t.nseg, 128)), dim3(128), 0, st,
@@ -1207,7 +1040,7 @@ int msm_fix_long(gm_ctx* ctx, MsmTail& t, uint32_t maxspan) {
   hipStream_t st = ctx->stream;
   const size_t nslices = (t.M + t.K - 1) / t.K;
   if constexpr (PairSel<DF>::ok) {
-    if (g2_pairs()) {
+    {
       for (uint32_t d = 0; (1u << d) < maxspan; d++)
         hipLaunchKernelGGL(PairSel<DF>::fix_tree(), dim3(blocks_for(2 * nslices, 128)), dim3(128), 0, st, t.keys,
                            t.offsets, t.total, t.K, (uint32_t)nslices, d, (uint32_t*)t.pfirst, FIX_SERIAL);
@@ -1270,11 +1103,10 @@ int msm_launch(gm_ctx* ctx, Arena& arena, const MsmPlan& plan, const void* point
   // L = 4: 0.36 / 1.74 / 6.05 -- the LDS bit-sum trees cost more per add than the
   // running sums.  So L grows (to 32) as long as k_msm_seg keeps >= 128K threads
   // (two waves per SIMD): 4 for 2^20 plain, 16 for the one-window 2^21 buckets
-  // of a precomputed 2^24 key.  GM_MSM_SEGL overrides (tuning).
-  static const int segl_env = getenv("GM_MSM_SEGL") ? atoi(getenv("GM_MSM_SEGL")) : 0;
+  // of a precomputed 2^24 key (segment lengths 4 / 8 re-measured in the pipelined
+  // loop, profiles/r05ai_segl_ab.txt).
   uint32_t Lwant = 4;
   while (Lwant < 32 && (size_t)t.Wr * t.nb / (2 * Lwant) >= (size_t(1) << 17)) Lwant *= 2;
-  if (segl_env > 0) Lwant = (uint32_t)segl_env;
   t.L = t.nb >= Lwant ? Lwant : t.nb;
   t.nseg = t.nb / t.L;
   // Entries per accumulation thread.  64 by default; 32 for G1 MSMs of at most
@@ -1283,8 +1115,9 @@ int msm_launch(gm_ctx* ctx, Arena& arena, const MsmPlan& plan, const void* point
   // accumulation alone drops 1.38-1.43 -> 1.34 ms and the pipelined MSM loop gains
   // 4-7 %, profiles/r04ae_slice_sweep.txt).  Larger MSMs keep 64 (Groth16 2^24:
   // 156.9 vs 159.3 ms at 32).  The long-span bound FIX_SERIAL * K stays above the
-  // fullest uniform bucket (64 entries at 2^20).  GM_MSM_SLICE overrides.
-  t.K = ctx->msm_slice ? (uint32_t)ctx->msm_slice : (!G2 && plan.M <= (size_t(1) << 25) ? 32u : 64u);
+  // fullest uniform bucket (64 entries at 2^20).  K % 4 == 0: the accumulation
+  // loads keys / values four entries at a time.
+  t.K = !G2 && plan.M <= (size_t(1) << 25) ? 32u : 64u;
   int rc;
   constexpr int WORDS = Coord<DF>::WORDS;  // u32 words of one gnark-layout coordinate
   static_assert(sizeof(HF) == 4 * WORDS, "host/device layout mismatch");
@@ -1306,64 +1139,41 @@ int msm_launch(gm_ctx* ctx, Arena& arena, const MsmPlan& plan, const void* point
   GM_HIP(hipMemsetAsync(errw.p, 0, 16, st));
   {
     GM_HIP(hipMemsetAsync(buckets.p, 0, sizeof(XYZZ<DF>) * (size_t)t.total, st));  // all-zero XYZZ = infinity
-    ProfScope ps(ctx, G2 ? "msm_accum_g2" : "msm_accum_g1", true);  // stamped by the launch
-    // G2 defaults to lane pairs; GM_MSM_ACCUM=prefetch|noprefetch selects the
-    // one-lane kernels instead (tuning / A-B); for G1, prefetch selects the
-    // three-wave prefetching kernel
-    static const char* ov = getenv("GM_MSM_ACCUM");
-    bool pair = G2 && g2_pairs();
-    const bool prefetch = ov && !strcmp(ov, "prefetch");
-    if constexpr (PairSel<DF>::ok) {
-      if (pair) {
-        hipExtLaunchKernelGGL(PairSel<DF>::kernel(t.K), dim3(blocks_for(2 * nslices, 128)), dim3(128), 0, st, ps.a,
-                              ps.b, 0, reinterpret_cast<const uint32_t*>(points_internal), (uint32_t)plan.npts,
-                              plan.keys, plan.vals, plan.offsets, t.total, t.K, buckets.as<uint32_t>(),
-                              pfirst.as<uint32_t>(), plast.as<uint32_t>(), errw.as<uint32_t>());
-      }
-    } else {
-      pair = false;
+    // async MSMs: this accumulation starts after the previous one (gm_ctx::acc_tail)
+    if (ctx->acc_chain) {
+      if (!ctx->acc_tail) GM_HIP(hipEventCreateWithFlags(&ctx->acc_tail, hipEventDisableTiming));
+      else GM_HIP(hipStreamWaitEvent(st, ctx->acc_tail, 0));
     }
-    if constexpr (kOneLane<DF>) {
-      if (!pair) {
-        static const bool acc_v4 = !getenv("GM_MSM_ACC_V4") || atoi(getenv("GM_MSM_ACC_V4")) != 0;
-        const bool v4 = acc_v4 && (t.K & 3) == 0;
-        auto accum = prefetch ? k_msm_accum_seg_pf<DF> : (G2 ? k_msm_accum_seg_g2<DF> : k_msm_accum_seg_pf<DF>);
-        if (!G2 && v4 && !ov) accum = k_msm_accum_seg_pf4<DF>;
-        if constexpr (AccumW4<DF>::ok) {
-          if (!prefetch) accum = k_msm_accum_seg<DF>;
-          if (ov && !strcmp(ov, "idx")) accum = k_msm_accum_seg_idx<DF>;
-          // default since r05: one mad chain per product in the G1 accumulation only
-          // (115 instead of 127 VGPRs; same box, isolated launch 1.306-1.318 vs
-          // 1.311-1.345 ms at 2^20, Groth16 2^24 within noise,
-          // profiles/r05e_acc_chain_ab.txt); GM_MSM_ACC_CHAIN=0: the split columns
-          static const bool acc_chain = !getenv("GM_MSM_ACC_CHAIN") || atoi(getenv("GM_MSM_ACC_CHAIN")) != 0;
-          if (acc_chain && !prefetch && !ov)
-            accum = v4 ? k_msm_accum_seg_ch<DF> : k_msm_accum_seg_ch1<DF>;  // v4: K % 4 == 0
-        }
-        hipExtLaunchKernelGGL(accum, dim3(blocks_for(nslices, 128)), dim3(128), 0, st, ps.a, ps.b, 0,
-                              reinterpret_cast<const uint32_t*>(points_internal), (uint32_t)plan.npts, plan.keys,
-                              plan.vals, plan.offsets, t.total, t.K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(),
-                              plast.as<XYZZ<DF>>(), errw.as<uint32_t>());
+    struct TailMark {  // recorded once the accumulation is queued
+      gm_ctx* c;
+      hipStream_t s;
+      ~TailMark() {
+        if (c->acc_chain) hipEventRecord(c->acc_tail, s);
       }
+    } tail_mark{ctx, st};
+    ProfScope ps(ctx, G2 ? "msm_accum_g2" : "msm_accum_g1", true);  // stamped by the launch
+    if constexpr (PairSel<DF>::ok) {
+      hipExtLaunchKernelGGL(PairSel<DF>::kernel(), dim3(blocks_for(2 * nslices, 128)), dim3(128), 0, st, ps.a, ps.b,
+                            0, reinterpret_cast<const uint32_t*>(points_internal), (uint32_t)plan.npts, plan.keys,
+                            plan.vals, plan.offsets, t.total, t.K, buckets.as<uint32_t>(), pfirst.as<uint32_t>(),
+                            plast.as<uint32_t>(), errw.as<uint32_t>());
+    } else {
+      hipExtLaunchKernelGGL(g1_accum_kernel<DF>(), dim3(blocks_for(nslices, 128)), dim3(128), 0, st, ps.a, ps.b, 0,
+                            reinterpret_cast<const uint32_t*>(points_internal), (uint32_t)plan.npts, plan.keys,
+                            plan.vals, plan.offsets, t.total, t.K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(),
+                            plast.as<XYZZ<DF>>(), errw.as<uint32_t>());
     }
   }
   {
     ProfScope ps(ctx, "msm_fixup");
-    bool done = false;
-    if constexpr (PairSel<DF>::ok) {
-      if (g2_pairs()) {
-        hipLaunchKernelGGL(PairSel<DF>::fixup(), dim3(blocks_for(2 * (size_t)t.total, 128)), dim3(128), 0, st,
-                           plan.offsets, t.total, t.K, buckets.as<uint32_t>(), pfirst.as<uint32_t>(),
-                           plast.as<uint32_t>(), errw.as<uint32_t>() + 1, FIX_SERIAL);
-        done = true;
-      }
-    }
-    if constexpr (kOneLane<DF>) {
-      if (!done)
-        hipLaunchKernelGGL(k_msm_fixup<DF>, dim3(blocks_for(t.total, 128)), dim3(128), 0, st, plan.offsets, t.total,
-                           t.K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>(),
-                           errw.as<uint32_t>() + 1);
-    }
+    if constexpr (PairSel<DF>::ok)
+      hipLaunchKernelGGL(PairSel<DF>::fixup(), dim3(blocks_for(2 * (size_t)t.total, 128)), dim3(128), 0, st,
+                         plan.offsets, t.total, t.K, buckets.as<uint32_t>(), pfirst.as<uint32_t>(),
+                         plast.as<uint32_t>(), errw.as<uint32_t>() + 1, FIX_SERIAL);
+    else
+      hipLaunchKernelGGL(k_msm_fixup<DF>, dim3(blocks_for(t.total, 128)), dim3(128), 0, st, plan.offsets, t.total,
+                         t.K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>(),
+                         errw.as<uint32_t>() + 1);
   }
   // Bucket reduction, launched speculatively: buckets spanning more than
   // FIX_SERIAL slices (skewed scalars) are only known once errw[1] (max span)
@@ -1493,26 +1303,13 @@ int msm_device_launch(gm_ctx* ctx, Arena& arena, const void* scalars_dev, const 
     glv = Glv<C>::ok && msm_glv_on(ctx, G2, n);
     if ((rc = ipts.alloc(arena, 2 * Coord<DF>::WORDS * sizeof(uint32_t) * n * (glv ? 2 : 1)))) return rc;
     ProfScope ps(ctx, "msm_convert_points");
-    // GM_MSM_CONVERT_LDS=0: the per-lane 64-B conversion kernels (A/B)
-    static const bool lds = !getenv("GM_MSM_CONVERT_LDS") || atoi(getenv("GM_MSM_CONVERT_LDS")) != 0;
     const uint32_t* src = reinterpret_cast<const uint32_t*>(points_dev);
-    if (lds) {
-      if (glv)
-        hipLaunchKernelGGL((k_msm_convert_points_lds<DF, true>), dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream,
-                           src, n, ipts.as<uint32_t>());
-      else
-        hipLaunchKernelGGL((k_msm_convert_points_lds<DF, false>), dim3(blocks_for(n, 256)), dim3(256), 0,
-                           ctx->stream, src, n, ipts.as<uint32_t>());
-    } else {
-      if constexpr (Glv<C>::ok) {
-        if (glv)
-          hipLaunchKernelGGL(k_msm_convert_points_glv<DF>, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream, src,
-                             n, ipts.as<uint32_t>());
-      }
-      if (!glv)
-        hipLaunchKernelGGL(k_msm_convert_points<DF>, dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream, src, n,
-                           ipts.as<uint32_t>());
-    }
+    if (glv)
+      hipLaunchKernelGGL((k_msm_convert_points_lds<DF, true>), dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream,
+                         src, n, ipts.as<uint32_t>());
+    else
+      hipLaunchKernelGGL((k_msm_convert_points_lds<DF, false>), dim3(blocks_for(n, 256)), dim3(256), 0, ctx->stream,
+                         src, n, ipts.as<uint32_t>());
     pts = ipts.p;
   }
   MsmPlan plan;

@@ -26,6 +26,21 @@
 
 namespace gm {
 
+// LDS bytes one workgroup may allocate on `device` (queried once per device)
+static size_t device_lds_per_block(int device) {
+  static std::mutex mu;
+  static std::map<int, size_t> cache;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find(device);
+  if (it != cache.end()) return it->second;
+  int v = 0;
+  if (hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess) {
+    (void)hipGetLastError();
+    v = 64 << 10;
+  }
+  return cache[device] = (size_t)v;
+}
+
 static __global__ void __launch_bounds__(1024) k_msm_s1_scan(const uint32_t* __restrict__ ccount, uint32_t NC,
                                                              uint32_t T, uint32_t psz, uint32_t* __restrict__ cbase,
                                                              uint32_t* __restrict__ ccursor,
@@ -433,12 +448,13 @@ int msm_sort_digits(gm_ctx* ctx, Arena& arena, const SortGeom& g, size_t n, uint
   // bins one pass-1 block touches: its window's own nb >> shift in the plain layout
   const uint32_t nh = (!shared_stride && (1u << shift) <= nb) ? nb >> shift : g.NS;
   // staged (coalesced-write) pass 1 while its LDS fits: 64 KB of entries plus
-  // three words per touched bin (GM_MSM_S1_STAGED=0: the direct scatter, A/B)
-  static const bool s1_staged = !getenv("GM_MSM_S1_STAGED") || atoi(getenv("GM_MSM_S1_STAGED")) != 0;
-  if (s1_staged && nh <= 4096) {
-    const size_t lds = 8 * (size_t)S1_PTS + sizeof(uint32_t) * (3 * (size_t)nh + 17);
+  // three words per touched bin (up to ~112 KB at 4,096 bins: gfx950 has 160 KB
+  // per workgroup; a device with less takes the direct scatter)
+  const size_t lds = 8 * (size_t)S1_PTS + sizeof(uint32_t) * (3 * (size_t)nh + 17);
+  if (nh <= 4096 && lds <= device_lds_per_block(ctx->device)) {
     hipLaunchKernelGGL(k_msm_s1_scatter_st<S1_PPT>, dim3(blocks_for(n, S1_PTS), W), dim3(S_THREADS), lds, st, dig,
                        (uint32_t)n, nb, shared_stride, shift, g.NS, nh, scursor.as<uint32_t>(), tmp.as<uint64_t>());
+    GM_HIP(hipGetLastError());
   } else {
     hipLaunchKernelGGL(k_msm_s1_scatter, dim3(blocks_for(n, S1_PTS), W), dim3(S_THREADS), 2 * sizeof(uint32_t) * nh,
                        st, dig, (uint32_t)n, nb, shared_stride, shift, g.NS, nh, scursor.as<uint32_t>(),

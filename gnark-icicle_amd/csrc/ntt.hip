@@ -77,11 +77,12 @@ GM_DEV void bfly_index(int q, int lm, int lgB, int& jj, int& ol, int& grp) {
   }
 }
 
-// TPB threads per tile (256, or 512: one butterfly per thread and stage);
-// SWG: sub-transform twiddles read through the cache instead of staged in LDS
-// (36 KiB instead of 41.5 KiB of LDS per block: four blocks per CU).
-template <class P, bool DIT, int TPB = NTT_TPB, bool SWG = false>
-__global__ void __launch_bounds__(TPB) k_ntt_pass(Fe<P>* __restrict__ data, int logn, int lo,
+// Radix-2 pass: the stages of one odd-t pass below t = 2 (k_ntt_pass4 runs the
+// others).  Sub-transform twiddles are read through the cache, not staged in LDS
+// (36 KiB of LDS per block: four blocks per CU; 1.5-2 % at 2^24 in r03,
+// profiles/r03m_ntt_swg_ab.txt).
+template <class P, bool DIT>
+__global__ void __launch_bounds__(NTT_TPB) k_ntt_pass(Fe<P>* __restrict__ data, int logn, int lo,
                                                       int t, const Fe<P>* __restrict__ tw,
                                                       const Fe<P>* __restrict__ sub,
                                                       const Fe<P>* __restrict__ pre,
@@ -90,7 +91,7 @@ __global__ void __launch_bounds__(TPB) k_ntt_pass(Fe<P>* __restrict__ data, int 
                                                       const Fe<P>* __restrict__ pc) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   Fe<P>* X = reinterpret_cast<Fe<P>*>(smem_raw);   // [T][B]
-  Fe<P>* SWl = X + NTT_TILE;                        // [T/2]
+  constexpr int TPB = NTT_TPB;
   const int T = 1 << t;
   const int lgB = NTT_TILE_LOG - t;
   const int B = 1 << lgB;
@@ -98,9 +99,7 @@ __global__ void __launch_bounds__(TPB) k_ntt_pass(Fe<P>* __restrict__ data, int 
   const size_t o0 = (size_t)blockIdx.x * B;
   const size_t lomask = ((size_t)1 << lo) - 1;
 
-  if (!SWG)
-    for (int x = threadIdx.x; x < T / 2; x += TPB) SWl[x] = ld_tab(sub, x);
-  const Fe<P>* __restrict__ SW = SWG ? sub : SWl;
+  const Fe<P>* __restrict__ SW = sub;
 
   // load (j, o) -> X[j*B + o]
   for (int q = threadIdx.x; q < NTT_TILE; q += TPB) {
@@ -319,7 +318,12 @@ GM_DEV Fe<P> ntt_tw(const Fe<P>* __restrict__ sub, int i) {
 // products of a round: one mad chain each (CH) or the compiler's split columns.
 // A difference that only feeds a product is formed carry-free (fe_sub_cf: value
 // below a + K p with K one above fe_sub_lz's, every product input < 33 p^2 < R' p).
-#define MUL(x, y) (CH ? fe_mul_lz_chain(x, y) : fe_mul_lz(x, y))
+// NTT_BFLY_CHAIN: the butterflies' chain level (1: one chain per column; the
+// load / store products take CH itself)
+#ifndef NTT_BFLY_CHAIN
+#define NTT_BFLY_CHAIN 1
+#endif
+#define MUL(x, y) (CH ? fe_mul<P, false, NTT_BFLY_CHAIN>(x, y) : fe_mul_lz(x, y))
 // DIF radix-2 butterfly pair of one round: (u, v) -> (u + v, (u - v + Kp) w)
 template <class P, int CH>
 GM_DEV void r4_dif(Fe<P> (&e)[4], const Fe<P>& t1, const Fe<P>& t2, const Fe<P>& t3) {
@@ -962,23 +966,7 @@ static int run_passes(gm_ctx* ctx, NttDomain<C>* d, Fe<typename C::Fr>* a, bool 
                       const NttFuse<typename C::Fr>& fz) {
   using Fr = typename C::Fr;
   hipStream_t st = ctx->stream;
-  // Twiddles are read through the cache by default (LDS holds the tile only:
-  // four blocks per CU; 1.5-2 % faster at 2^24 with the interleaved butterflies,
-  // profiles/r03m_ntt_swg_ab.txt); GM_NTT_SWG=0 stages them in LDS.
-  // GM_NTT_TPB=512: one butterfly per thread and stage (no gain measured).
-  static const int tpb = getenv("GM_NTT_TPB") ? atoi(getenv("GM_NTT_TPB")) : NTT_TPB;
-  static const bool swg = getenv("GM_NTT_SWG") ? atoi(getenv("GM_NTT_SWG")) != 0 : true;
-  // radix-4 passes (k_ntt_pass4) by default; GM_NTT_R4=0: the radix-2 kernel (A/B)
-  static const bool r4 = getenv("GM_NTT_R4") ? atoi(getenv("GM_NTT_R4")) != 0 : true;
-  // strict mad chains in every product (fe_mul CHAIN level 2: each mad adds onto the
-  // previous one, no column summed in halves and joined with v_lshl_add_u64; per-
-  // column chains (level 1, r04) took 2.20-2.23 -> 2.10-2.12 ms per 2^24 transform,
-  // profiles/r04h_ntt_ab.txt, strict ones 2.11 -> 2.05-2.06, r05an_strict_chain_ab.txt);
-  // GM_NTT_CHAIN=0: the compiler's schedule (A/B)
-  static const bool r4chain = getenv("GM_NTT_CHAIN") ? atoi(getenv("GM_NTT_CHAIN")) != 0 : true;
-  // growing bounds: bit 0 DIF passes (r4_dif_grow), bit 1 DIT passes (r4_dit_grow)
-  static const int r4grow = getenv("GM_NTT_GROW") ? atoi(getenv("GM_NTT_GROW")) : 3;
-  const size_t smem = sizeof(Fe<Fr>) * (NTT_TILE + (swg ? 0 : (1 << (NTT_TMAX - 1))));
+  const size_t smem = sizeof(Fe<Fr>) * NTT_TILE;
   const int np = (int)d->passes.size();
   for (int k = 0; k < np; k++) {
     const int pi = dit ? np - 1 - k : k;
@@ -991,19 +979,18 @@ static int run_passes(gm_ctx* ctx, NttDomain<C>* d, Fe<typename C::Fr>* a, bool 
     const size_t B = NTT_TILE >> ps.t;
     const unsigned grid = (unsigned)((nother + B - 1) / B);
     ProfScope pscope(ctx, "ntt_pass");
-    if (r4 && ps.t >= 2) {
-      auto k4 = dit ? (r4chain ? k_ntt_pass4<Fr, true, 2> : k_ntt_pass4<Fr, true>)
-                    : (r4chain ? k_ntt_pass4<Fr, false, 2> : k_ntt_pass4<Fr, false>);
-      hipLaunchKernelGGL(k4, dim3(grid), dim3(NTT_TPB),
-                         sizeof(Fe<Fr>) * NTT_TILE, st, a, d->logn, ps.lo, ps.t, r4grow, tw, sub, first ? fz.pre : nullptr,
-                         last ? fz.post : nullptr, first ? fz.pb : nullptr, first ? fz.pc : nullptr);
+    // radix-4 passes for t >= 2 with strict mad chains in the load / store products
+    // (fe_mul CHAIN level 2, profiles/r05an_strict_chain_ab.txt) and growing bounds
+    // in both pass kinds (r4_dif_grow / r4_dit_grow, r04g / r04af)
+    if (ps.t >= 2) {
+      auto k4 = dit ? k_ntt_pass4<Fr, true, 2> : k_ntt_pass4<Fr, false, 2>;
+      hipLaunchKernelGGL(k4, dim3(grid), dim3(NTT_TPB), smem, st, a, d->logn, ps.lo, ps.t, 3, tw, sub,
+                         first ? fz.pre : nullptr, last ? fz.post : nullptr, first ? fz.pb : nullptr,
+                         first ? fz.pc : nullptr);
       continue;
     }
     auto kern = dit ? k_ntt_pass<Fr, true> : k_ntt_pass<Fr, false>;
-    if (tpb == 512) kern = dit ? (swg ? k_ntt_pass<Fr, true, 512, true> : k_ntt_pass<Fr, true, 512>)
-                               : (swg ? k_ntt_pass<Fr, false, 512, true> : k_ntt_pass<Fr, false, 512>);
-    else if (swg) kern = dit ? k_ntt_pass<Fr, true, NTT_TPB, true> : k_ntt_pass<Fr, false, NTT_TPB, true>;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(tpb == 512 ? 512 : NTT_TPB), smem, st, a, d->logn, ps.lo, ps.t, tw, sub,
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(NTT_TPB), smem, st, a, d->logn, ps.lo, ps.t, tw, sub,
                        first ? fz.pre : nullptr, last ? fz.post : nullptr, first ? fz.pb : nullptr,
                        first ? fz.pc : nullptr);
   }

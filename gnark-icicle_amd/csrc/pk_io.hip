@@ -226,6 +226,16 @@ struct gm_g16_stage {
   hipEvent_t ev[SLOTS] = {};
   bool used[SLOTS] = {};
   int next = 0;
+  // Indexed puts are records (u32 element, u32 vector, 32-B value) gathered in
+  // the open ring slot: a put of one element (a solver level of one wire, the
+  // squaring chain of groth16_test.go:120-156) costs its record copy, not a slot,
+  // a copy and a launch.  The slot is flushed when full, when it holds FLUSH_AT
+  // records at the end of a put (so the copies still overlap Solve), before a
+  // range put and before the prove.
+  static constexpr size_t REC_PER = (SLOT - 16) / 40 & ~size_t(3);
+  static constexpr size_t FLUSH_AT = size_t(1) << 16;
+  int open = -1;
+  size_t open_cnt = 0;
   int take(int* k) {
     *k = next;
     next = (next + 1) % SLOTS;
@@ -233,6 +243,7 @@ struct gm_g16_stage {
     used[*k] = true;
     return GM_OK;
   }
+  int flush();
   ~gm_g16_stage() {
     for (int i = 0; i < SLOTS; i++) {
       if (ev[i]) {
@@ -254,19 +265,48 @@ bool getenv_flag_off(const char* name) {
   return v && atoi(v) == 0;
 }
 
-// dst[idx[j]] = val[j] (32-byte Fr)
+// the stage's four vectors, passed by value to the scatter
+struct StageDst {
+  uint4* v[4];
+  size_t len[4];
+};
+// dst[rec[j].y][rec[j].x] = val[j] (32-byte Fr)
 // (gm_g16_stage_put_indexed checks every index on the host before the copy;
-// the i < len test only keeps a bad launch from writing out of bounds)
-__global__ void k_scatter_fr(const uint32_t* __restrict__ idx, const uint4* __restrict__ val, size_t k, size_t len,
-                             uint4* __restrict__ dst) {
+// the bounds test only keeps a bad launch from writing out of bounds)
+__global__ void k_scatter_fr(const uint2* __restrict__ rec, const uint4* __restrict__ val, size_t k, StageDst d) {
   const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= k) return;
-  const size_t i = idx[j];
-  if (i >= len) return;
-  dst[2 * i] = val[2 * j];
-  dst[2 * i + 1] = val[2 * j + 1];
+  const uint2 r = rec[j];
+  if (r.y > 3 || r.x >= d.len[r.y]) return;
+  uint4* dst = d.v[r.y];
+  dst[2 * (size_t)r.x] = val[2 * j];
+  dst[2 * (size_t)r.x + 1] = val[2 * j + 1];
 }
 }  // namespace
+
+// queue the open slot's records: copy to the slot's device staging, scatter
+int gm_g16_stage::flush() {
+  if (open < 0) return GM_OK;
+  const int s = open;
+  const size_t cnt = open_cnt;
+  open = -1;
+  open_cnt = 0;
+  if (cnt == 0) return GM_OK;
+  GM_HIP(hipSetDevice(ctx->device));
+  StageDst d;
+  for (int v = 0; v < 4; v++) {
+    d.v[v] = (uint4*)vec[v];
+    d.len[v] = len[v];
+  }
+  char* dv = (char*)dev[s] + 8 * REC_PER;
+  GM_HIP(hipMemcpyAsync(dev[s], host[s], 8 * cnt, hipMemcpyHostToDevice, ctx->copy));
+  GM_HIP(hipMemcpyAsync(dv, (char*)host[s] + 8 * REC_PER, 32 * cnt, hipMemcpyHostToDevice, ctx->copy));
+  hipLaunchKernelGGL(k_scatter_fr, dim3(blocks_for(cnt, 256)), dim3(256), 0, ctx->copy, (const uint2*)dev[s],
+                     (const uint4*)dv, cnt, d);
+  GM_HIP(hipGetLastError());
+  GM_HIP(hipEventRecord(ev[s], ctx->copy));
+  return GM_OK;
+}
 
 extern "C" {
 
@@ -486,8 +526,16 @@ int gm_g16_pk_load_cache(gm_ctx* ctx, int fd, gm_g16_pk** out) {
 // ---- staged inputs ----------------------------------------------------------
 }  // extern "C"
 
+// a key's parked stage leaves its context's list (reused or released)
+static void spare_unlist(gm_g16_pk* pk) {
+  if (!pk->spare_stage) return;
+  auto& v = pk->spare_stage->ctx->spare_keys;
+  v.erase(std::remove(v.begin(), v.end(), pk), v.end());
+}
+
 void gm::stage_spare_release(gm_g16_pk* pk) {
   if (pk->spare_stage) {
+    spare_unlist(pk);
     delete pk->spare_stage;
     pk->spare_stage = nullptr;
   }
@@ -505,10 +553,13 @@ int gm_g16_stage_begin(gm_ctx* ctx, gm_g16_pk* pk, size_t nb_constraints, gm_g16
   GM_HIP(hipSetDevice(ctx->device));
   if (gm_g16_stage* sp = pk->spare_stage; sp && sp->ctx == ctx) {
     // the key's buffers of a previous proof (gm_g16_stage_free parked them)
+    spare_unlist(pk);
     pk->spare_stage = nullptr;
     sp->nc = nb_constraints;
     for (int v = 0; v < 3; v++) sp->len[v] = nb_constraints;
     sp->next = 0;
+    sp->open = -1;
+    sp->open_cnt = 0;
     for (bool& u : sp->used) u = false;
     *out = sp;
     return GM_OK;
@@ -547,13 +598,14 @@ int gm_g16_stage_put_range(gm_g16_stage* st, int which, size_t lo, size_t count,
   }
   gm_ctx* ctx = st->ctx;
   gm::CtxLock g(ctx);
+  if (int rc = st->flush()) return rc;  // earlier indexed puts land first
   GM_HIP(hipSetDevice(ctx->device));
   const size_t per = gm_g16_stage::SLOT / 32;
   for (size_t o = 0; o < count; o += per) {
     const size_t cnt = std::min(per, count - o);
     int k;
     if (int rc = st->take(&k)) return rc;
-    par_memcpy(st->host[k], (const char*)host_src + 32 * o, 32 * cnt, h2d_fill_threads());
+    par_memcpy(st->host[k], (const char*)host_src + 32 * o, 32 * cnt, H2D_FILL_THREADS);
     GM_HIP(hipMemcpyAsync((char*)st->vec[which] + 32 * (lo + o), st->host[k], 32 * cnt, hipMemcpyHostToDevice,
                           ctx->copy));
     GM_HIP(hipEventRecord(st->ev[k], ctx->copy));
@@ -563,36 +615,36 @@ int gm_g16_stage_put_range(gm_g16_stage* st, int which, size_t lo, size_t count,
 
 int gm_g16_stage_put_indexed(gm_g16_stage* st, int which, const void* host_base, const uint32_t* idx, size_t k) {
   if (!st || which < 0 || which > 3 || (k && (!host_base || !idx))) return GM_ERR_INVALID;
-  gm_ctx* ctx = st->ctx;
-  gm::CtxLock g(ctx);
-  GM_HIP(hipSetDevice(ctx->device));
-  // a slot holds per records: per u32 indices, then per 32-B values (16-B aligned)
-  const size_t per = (gm_g16_stage::SLOT - 16) / 36 & ~size_t(3);
+  if (k == 0) return GM_OK;
+  std::lock_guard<std::recursive_mutex> g(st->ctx->mu);  // nothing queued on ctx->stream
+  constexpr size_t per = gm_g16_stage::REC_PER;
   const char* base = (const char*)host_base;
-  for (size_t o = 0; o < k; o += per) {
-    const size_t cnt = std::min(per, k - o);
-    int s;
-    if (int rc = st->take(&s)) return rc;
-    uint32_t* hi = (uint32_t*)st->host[s];
-    char* hv = (char*)st->host[s] + 4 * per;
-    for (size_t j = 0; j < cnt; j++) {
-      const uint32_t i = idx[o + j];
-      if (i >= st->len[which]) {
+  const size_t lim = st->len[which];
+  for (size_t o = 0; o < k;) {
+    if (st->open < 0) {
+      int s;
+      if (int rc = st->take(&s)) return rc;
+      st->open = s;
+    }
+    uint2* hr = (uint2*)st->host[st->open];
+    char* hv = (char*)st->host[st->open] + 8 * per;
+    size_t j = st->open_cnt;
+    const size_t end = std::min(k, o + (per - j));
+    for (; o < end; o++, j++) {
+      const uint32_t i = idx[o];
+      if (i >= lim) {
+        st->open_cnt = j;
         set_error("stage: index outside the vector");
         return GM_ERR_INVALID;
       }
-      hi[j] = i;
+      hr[j] = make_uint2(i, (uint32_t)which);
       memcpy(hv + 32 * j, base + 32 * (size_t)i, 32);
     }
-    uint32_t* di = (uint32_t*)st->dev[s];
-    char* dv = (char*)st->dev[s] + 4 * per;
-    GM_HIP(hipMemcpyAsync(di, hi, 4 * cnt, hipMemcpyHostToDevice, ctx->copy));
-    GM_HIP(hipMemcpyAsync(dv, hv, 32 * cnt, hipMemcpyHostToDevice, ctx->copy));
-    hipLaunchKernelGGL(k_scatter_fr, dim3(blocks_for(cnt, 256)), dim3(256), 0, ctx->copy, di, (const uint4*)dv, cnt,
-                       st->len[which], (uint4*)st->vec[which]);
-    GM_HIP(hipGetLastError());
-    GM_HIP(hipEventRecord(st->ev[s], ctx->copy));
+    st->open_cnt = j;
+    if (j == per)
+      if (int rc = st->flush()) return rc;
   }
+  if (st->open_cnt >= gm_g16_stage::FLUSH_AT) return st->flush();
   return GM_OK;
 }
 
@@ -601,6 +653,7 @@ int gm_g16_stage_prove(gm_g16_stage* st, const void* r, const void* s, void* ar_
   gm_ctx* ctx = st->ctx;
   {
     gm::CtxLock g(ctx);
+    if (int rc = st->flush()) return rc;
     GM_HIP(hipSetDevice(ctx->device));
     GM_HIP(hipStreamSynchronize(ctx->copy));
   }
@@ -619,6 +672,7 @@ int gm_g16_stage_prove_r1cs(gm_g16_stage* st, const gm_r1cs* r1, const void* r, 
   }
   {
     gm::CtxLock g(ctx);
+    if (int rc = st->flush()) return rc;
     GM_HIP(hipSetDevice(ctx->device));
     GM_HIP(hipStreamSynchronize(ctx->copy));
   }
@@ -630,6 +684,8 @@ int gm_g16_stage_prove_r1cs(gm_g16_stage* st, const gm_r1cs* r1, const void* r, 
 int gm_g16_stage_free(gm_g16_stage* st) {
   if (!st) return GM_OK;
   gm::CtxLock g(st->ctx);
+  st->open = -1;  // records not yet queued are dropped with the stage
+  st->open_cnt = 0;
   hipSetDevice(st->ctx->device);
   hipStreamSynchronize(st->ctx->copy);
   // Park the buffers with the key for its next proof (one spare per key): a
@@ -637,6 +693,7 @@ int gm_g16_stage_free(gm_g16_stage* st) {
   // memory.  The prove that used them has returned, so nothing reads them.
   if (!st->pk->spare_stage && !getenv_flag_off("GM_G16_STAGE_REUSE")) {
     st->pk->spare_stage = st;
+    st->ctx->spare_keys.push_back(st->pk);
     return GM_OK;
   }
   delete st;

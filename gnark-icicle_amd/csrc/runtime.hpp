@@ -19,6 +19,7 @@
 namespace gm {
 
 void set_error(const std::string& msg);
+std::string last_error();  // this thread's last error message
 size_t fp_bytes(int curve);  // bytes of one base-field element (gnark layout)
 
 #define GM_HIP(call)                                                                      \
@@ -69,8 +70,7 @@ struct gm_ctx {
   // cached NTT domains: key = curve*64 + logn
   std::map<int, void*> ntt_domains;
   int msm_c_override = 0;
-  int msm_slice = 0;  // entries per thread in the bucket accumulation (0 = default)
-  int msm_glv = -1;   // GLV split of plain MSMs: -1 = environment default, 0 off, 1 on
+  int msm_glv = -1;   // GLV split of plain MSMs: -1 = default (n <= 2^21), 0 off, 1 on
   // workspace arena (stack-discipline scopes), plus two more for MSMs whose host
   // tail is deferred (pipelined MSMs: gm_msm_async, the Groth16 MSM sequence)
   gm::ArenaState arena;
@@ -88,6 +88,12 @@ struct gm_ctx {
   // the device -- one's sort / reduction (HBM / latency-bound) runs beside
   // another's accumulation (VALU-bound).  Created on first use.
   hipStream_t slot_stream[MSM_SLOTS] = {};
+  // Bucket accumulations of in-flight async MSMs run one after another: each one's
+  // slot stream waits on `acc_tail`, recorded after the previous accumulation.
+  // Only the accumulation is ordered; the sorts and reductions of the other MSMs
+  // still run beside it.  `acc_chain` is set while gm_msm_async queues its MSM.
+  hipEvent_t acc_tail = nullptr;
+  bool acc_chain = false;
   // the Groth16 prove's second MSM stream (GM_G16_MSM_STREAMS=1), created on first use
   hipStream_t g16_stream = nullptr;
   // gm_msm_async handles not yet waited for: gm_destroy drains their device work,
@@ -115,6 +121,9 @@ struct gm_ctx {
   static constexpr size_t H2D_SLOT = size_t(32) << 20;
   void* h2d_pin[H2D_SLOTS] = {};
   hipEvent_t h2d_ev[H2D_SLOTS] = {};
+  // keys holding a parked stage of this context (gm_g16_stage_free): gm_trim
+  // releases those stages' buffers
+  std::vector<gm_g16_pk*> spare_keys;
 };
 
 namespace gm {
@@ -260,12 +269,8 @@ inline void par_memcpy(void* dst, const void* src, size_t len, int nt) {
   memcpy(dst, src, std::min(part, len));
   for (auto& w : ws) w.join();
 }
-// threads per pinned-slot fill: GM_G16_H2D_THREADS (1..16), default 4
-inline int h2d_fill_threads() {
-  static const int n =
-      getenv("GM_G16_H2D_THREADS") ? std::max(1, std::min(16, atoi(getenv("GM_G16_H2D_THREADS")))) : 4;
-  return n;
-}
+// threads per pinned-slot fill (profiles/r05l_host_h_incremental_ab.txt)
+constexpr int H2D_FILL_THREADS = 4;
 
 // A deferred-tail arena slot of the context (at most MSM_SLOTS MSMs in flight).
 // ctx->stream temporarily replaced (all MSM code queues on ctx->stream)

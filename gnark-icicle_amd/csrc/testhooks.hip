@@ -1,6 +1,9 @@
 // Element-wise test hooks for the device field / curve layer (used by the
 // parity tests to pin each arithmetic primitive against the oracle).  Not on
 // the proving path.
+#include <chrono>
+#include <vector>
+
 #include "curves.hpp"
 #include "runtime.hpp"
 #include "../../include/gnark_mi355x_testhooks.h"
@@ -120,4 +123,56 @@ int gm_test_point_op(gm_ctx* ctx, int curve, int g2, int op, const void* a_dev, 
   return g2 ? point_op_t<CurveBLS12377, true>(ctx, op, a_dev, b_dev, out_dev, n)
             : point_op_t<CurveBLS12377, false>(ctx, op, a_dev, b_dev, out_dev, n);
 }
+}
+
+/* The solver-side cost of staging the reference benchmark circuit's level shape
+ * (backend/groth16/groth16_test.go:120-156: a chain of squarings; the solver runs
+ * it as one one-instruction level after another, constraint/bn254/solver.go:
+ * 471-484).  Level j finishes constraint j and solves wire nb_inputs + j (the
+ * last level, the final assertion, solves no wire).  mode 0: one put per level
+ * and vector; mode 1: the Go hook's pattern (integration/go/icicle_bn254/
+ * staged.go): ids appended to pending lists, handed over every `flush_at` ids and
+ * at the end.  abc = 0: wires only (resident constraint system).  The put range
+ * of the witness inputs comes first.  *ns_per_level = host time / levels. */
+extern "C" int gm_test_stage_replay_chain(gm_g16_stage* st, const void* wires, size_t nb_inputs, const void* a,
+                                          const void* b, const void* c, size_t nb_constraints, int mode, int abc,
+                                          size_t flush_at, double* ns_per_level) {
+  if (!st || !wires || !ns_per_level || (abc && (!a || !b || !c)) || nb_constraints == 0 || flush_at == 0)
+    return GM_ERR_INVALID;
+  const auto t0 = std::chrono::steady_clock::now();
+  int rc = gm_g16_stage_put_range(st, GM_STAGE_WIRES, 0, nb_inputs, wires);
+  std::vector<uint32_t> pw, pc;
+  pw.reserve(flush_at);
+  pc.reserve(flush_at);
+  auto put_abc = [&](const uint32_t* ids, size_t k) {
+    int r = gm_g16_stage_put_indexed(st, GM_STAGE_A, a, ids, k);
+    if (!r) r = gm_g16_stage_put_indexed(st, GM_STAGE_B, b, ids, k);
+    if (!r) r = gm_g16_stage_put_indexed(st, GM_STAGE_C, c, ids, k);
+    return r;
+  };
+  for (size_t j = 0; j < nb_constraints && !rc; j++) {
+    const uint32_t cid = (uint32_t)j, wid = (uint32_t)(nb_inputs + j);
+    const bool solves = j + 1 < nb_constraints;
+    if (mode == 0) {
+      if (solves) rc = gm_g16_stage_put_indexed(st, GM_STAGE_WIRES, wires, &wid, 1);
+      if (!rc && abc) rc = put_abc(&cid, 1);
+      continue;
+    }
+    if (solves) pw.push_back(wid);
+    if (pw.size() >= flush_at) {
+      rc = gm_g16_stage_put_indexed(st, GM_STAGE_WIRES, wires, pw.data(), pw.size());
+      pw.clear();
+    }
+    if (!abc || rc) continue;
+    pc.push_back(cid);
+    if (pc.size() >= flush_at) {
+      rc = put_abc(pc.data(), pc.size());
+      pc.clear();
+    }
+  }
+  if (!rc && !pw.empty()) rc = gm_g16_stage_put_indexed(st, GM_STAGE_WIRES, wires, pw.data(), pw.size());
+  if (!rc && !pc.empty()) rc = put_abc(pc.data(), pc.size());
+  *ns_per_level = std::chrono::duration<double, std::nano>(std::chrono::steady_clock::now() - t0).count() /
+                  (double)nb_constraints;
+  return rc;
 }

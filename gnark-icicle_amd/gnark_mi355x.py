@@ -56,7 +56,7 @@ SYMBOLS = [
     "gm_g16_prove_r1cs", "gm_g16_stage_prove_r1cs",
 ]
 # test-only library (include/gnark_mi355x_testhooks.h, libgnark_mi355x_testhooks.so)
-TEST_SYMBOLS = ["gm_test_field_op", "gm_test_point_op"]
+TEST_SYMBOLS = ["gm_test_field_op", "gm_test_point_op", "gm_test_stage_replay_chain"]
 TESTHOOKS_PATH = os.path.join(os.path.dirname(LIB_PATH), "libgnark_mi355x_testhooks.so")
 
 
@@ -82,6 +82,7 @@ def load_testhooks(path: str = None):
     vp, sz, i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
     T.gm_test_field_op.argtypes = [vp, i, i, i, vp, vp, vp, sz]
     T.gm_test_point_op.argtypes = [vp, i, i, i, vp, vp, vp, sz]
+    T.gm_test_stage_replay_chain.argtypes = [vp, vp, sz, vp, vp, vp, sz, i, i, sz, ctypes.POINTER(ctypes.c_double)]
     _testhooks = T
     return T
 
@@ -787,6 +788,22 @@ class Stage:
         b = _buf(base)
         ix = np.ascontiguousarray(np.asarray(idx, dtype=np.uint32))
         _check(load_library().gm_g16_stage_put_indexed(self.handle, which, _p(b), ix.ctypes.data, ix.size))
+
+    def replay_chain(self, wires, nb_inputs: int, nb_constraints: int, abc=None, coalesce=True,
+                     flush_at: int = 1 << 16) -> float:
+        """Test hook (gm_test_stage_replay_chain): stages the squaring chain's
+        level shape -- level j finishes constraint j and solves wire nb_inputs + j
+        -- one put per level (coalesce=False) or gathered as the Go level hook
+        does.  abc = (a, b, c) host vectors to stage as well.  Returns host ns per
+        level."""
+        w = _buf(wires)
+        bufs = [_buf(x) for x in abc] if abc is not None else []
+        ptrs = [_p(x) for x in bufs] if bufs else [None, None, None]
+        ns = ctypes.c_double()
+        _check(load_testhooks().gm_test_stage_replay_chain(self.handle, _p(w), nb_inputs, ptrs[0], ptrs[1], ptrs[2],
+                                                           nb_constraints, 1 if coalesce else 0, 1 if bufs else 0,
+                                                           flush_at, ctypes.byref(ns)))
+        return ns.value
 
     def prove(self, r: bytes, s: bytes):
         R, S = _buf(r), _buf(s)

@@ -54,7 +54,9 @@ int gm_destroy(gm_ctx* ctx);
 int gm_synchronize(gm_ctx* ctx);
 /* Releases the device memory a context keeps for reuse between calls: the
  * workspace arenas, the a / b / c input buffer of host-input proves (3 n Fr,
- * 1.5 GB at 2^24), the pinned H2D ring and the cached NTT domain tables.  All
+ * 1.5 GB at 2^24), the pinned H2D ring, the cached NTT domain tables and the
+ * staging buffers parked with keys by gm_g16_stage_free (3 n + nb_wires Fr plus
+ * 64 MiB pinned and 64 MiB device per key).  All
  * are re-created on demand by the next call that needs them.  Refused
  * (GM_ERR_INVALID) while gm_msm_async MSMs are pending.  Call it before
  * uploading a key whose GM_PK_PRECOMPUTE_AUTO decision should see that memory
@@ -386,7 +388,11 @@ int gm_g16_pk_load_cache(gm_ctx* ctx, int fd, gm_g16_pk** out);
  * prove consumes a, b, c (one proof per stage).  gm_g16_stage_free keeps the
  * stage's device vectors and pinned ring with the key (one spare per key,
  * released by gm_g16_pk_free), and the next gm_g16_stage_begin on the same
- * context reuses them: no allocation per proof (GM_G16_STAGE_REUSE=0: off). */
+ * context reuses them: no allocation per proof (GM_G16_STAGE_REUSE=0: off).
+ * Indexed puts are gathered as records (element id, vector, value) in the open
+ * ring slot and queued when it holds 65,536 of them, when it is full, before a
+ * range put and before the prove: a put of one element (a solver level that
+ * solved one wire) costs its 40-byte record, not a copy and a launch. */
 typedef struct gm_g16_stage gm_g16_stage;
 #define GM_STAGE_A 0
 #define GM_STAGE_B 1

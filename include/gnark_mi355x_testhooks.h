@@ -20,6 +20,15 @@ int gm_test_field_op(gm_ctx* ctx, int curve, int kind, int op, const void* a_dev
 int gm_test_point_op(gm_ctx* ctx, int curve, int g2, int op, const void* a_dev,
                      const void* b_dev, void* out_dev, size_t n);
 
+/* Replays the level shape of the reference benchmark circuit (a chain of
+ * squarings: level j finishes constraint j and solves wire nb_inputs + j)
+ * through gm_g16_stage_put_indexed: mode 0 one put per level and vector, mode 1
+ * the Go level hook's gathering (a put every flush_at ids); abc = 0 stages the
+ * wires only.  Reports the host time per level. */
+int gm_test_stage_replay_chain(gm_g16_stage* st, const void* wires, size_t nb_inputs, const void* a,
+                               const void* b, const void* c, size_t nb_constraints, int mode, int abc,
+                               size_t flush_at, double* ns_per_level);
+
 #ifdef __cplusplus
 }
 #endif

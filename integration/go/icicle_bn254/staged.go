@@ -25,6 +25,14 @@ import (
 	"github.com/consensys/gnark/backend/accel/mi355x/gm"
 )
 
+// stagedFlushAt is how many solved ids a level hook gathers before it hands
+// them to the device stage in one call.  The reference's benchmark circuit
+// (backend/groth16/groth16_test.go:120-156, a chain of squarings) solves one
+// wire and one constraint per level (constraint/bn254/solver.go:471-484), so
+// at 2^24 a call per level would be 2^24 cgo calls inside Solve; gathered, a
+// level costs two appends.
+const stagedFlushAt = 1 << 16
+
 // stagedRun is one proof's staging area plus the first error a level hook hit.
 type stagedRun struct {
 	st        *gm.G16Stage
@@ -32,6 +40,38 @@ type stagedRun struct {
 	nbInputs  int      // witness wires [0, nbInputs): ONE, public, secret
 	inputsPut bool
 	perr      error
+	// ids solved by levels and not yet handed over; values / a, b, c are the
+	// solver's vectors, whose entries are final once their level is done
+	pendW, pendC []uint32
+	values       unsafe.Pointer
+	a, b, c      unsafe.Pointer
+}
+
+// flushWires hands the gathered wire ids to the stage.
+func (run *stagedRun) flushWires() error {
+	if len(run.pendW) == 0 {
+		return nil
+	}
+	err := run.st.PutIndexed(gm.StageWires, run.values, run.pendW)
+	run.pendW = run.pendW[:0]
+	return err
+}
+
+// flushConstraints hands the gathered constraint ids' a, b, c to the stage.
+func (run *stagedRun) flushConstraints() error {
+	if len(run.pendC) == 0 {
+		return nil
+	}
+	for _, v := range []struct {
+		which int
+		base  unsafe.Pointer
+	}{{gm.StageA, run.a}, {gm.StageB, run.b}, {gm.StageC, run.c}} {
+		if err := run.st.PutIndexed(v.which, v.base, run.pendC); err != nil {
+			return err
+		}
+	}
+	run.pendC = run.pendC[:0]
+	return nil
 }
 
 // beginStaged opens a staging area for nbConstraints constraints and returns
@@ -42,11 +82,13 @@ func (pk *ProvingKey) beginStaged(nbConstraints, nbInputs int, r1 *gm.R1CS) (*st
 	if err != nil {
 		return nil, nil, err
 	}
-	run := &stagedRun{st: st, r1: r1, nbInputs: nbInputs}
+	run := &stagedRun{st: st, r1: r1, nbInputs: nbInputs,
+		pendW: make([]uint32, 0, stagedFlushAt), pendC: make([]uint32, 0, stagedFlushAt)}
 	hook := func(cIDs []uint32, a, b, c unsafe.Pointer, wIDs []uint32, values unsafe.Pointer) {
 		if run.perr != nil {
 			return
 		}
+		run.values, run.a, run.b, run.c = values, a, b, c
 		if !run.inputsPut { // the witness wires are solved before the first level
 			if err := st.PutRange(gm.StageWires, 0, run.nbInputs, values); err != nil {
 				run.perr = err
@@ -54,20 +96,20 @@ func (pk *ProvingKey) beginStaged(nbConstraints, nbInputs int, r1 *gm.R1CS) (*st
 			}
 			run.inputsPut = true
 		}
-		if err := st.PutIndexed(gm.StageWires, values, wIDs); err != nil {
-			run.perr = err
-			return
+		run.pendW = append(run.pendW, wIDs...)
+		if len(run.pendW) >= stagedFlushAt {
+			if err := run.flushWires(); err != nil {
+				run.perr = err
+				return
+			}
 		}
 		if run.r1 != nil || len(cIDs) == 0 {
 			return
 		}
-		for _, v := range []struct {
-			which int
-			base  unsafe.Pointer
-		}{{gm.StageA, a}, {gm.StageB, b}, {gm.StageC, c}} {
-			if err := st.PutIndexed(v.which, v.base, cIDs); err != nil {
+		run.pendC = append(run.pendC, cIDs...) // cIDs is the solver's scratch: copied
+		if len(run.pendC) >= stagedFlushAt {
+			if err := run.flushConstraints(); err != nil {
 				run.perr = err
-				return
 			}
 		}
 	}
@@ -80,6 +122,13 @@ func (pk *ProvingKey) beginStaged(nbConstraints, nbInputs int, r1 *gm.R1CS) (*st
 func (run *stagedRun) prove(w []fr.Element, r, s *fr.Element, ar, bs, krs unsafe.Pointer) error {
 	if run.perr != nil {
 		return run.perr
+	}
+	// what the last levels gathered
+	if err := run.flushWires(); err != nil {
+		return err
+	}
+	if err := run.flushConstraints(); err != nil {
+		return err
 	}
 	if !run.inputsPut { // a system without levels: the hook never ran
 		if err := run.st.PutRange(gm.StageWires, 0, len(w), unsafe.Pointer(&w[0])); err != nil {

@@ -87,8 +87,12 @@ func CopyPointsToDevice(pts []curve.G1Affine, bytes int, out chan unsafe.Pointer
 // CopyG2PointsToDevice (icicle.go:125)
 func CopyG2PointsToDevice(pts []curve.G2Affine, bytes int, out chan unsafe.Pointer) {
 	var p unsafe.Pointer
-	must(C.gm_copy_points_to_device(context(), C.GM_BN254, 1, unsafe.Pointer(&pts[0]), C.size_t(len(pts)), &p),
-		"CopyG2PointsToDevice")
+	if len(pts) == 0 {
+		must(C.gm_malloc(context(), 16, &p), "CopyG2PointsToDevice")
+	} else {
+		must(C.gm_copy_points_to_device(context(), C.GM_BN254, 1, unsafe.Pointer(&pts[0]), C.size_t(len(pts)), &p),
+			"CopyG2PointsToDevice")
+	}
 	runtime.KeepAlive(pts)
 	out <- p
 }

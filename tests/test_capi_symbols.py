@@ -58,16 +58,16 @@ def test_test_hooks_live_outside_the_product_library(lib):
     assert "k_field_op" not in nm and "k_point_op" not in nm
 
 
-def test_library_sets_hw_queue_default_at_load():
-    """The library's load-time constructor gives the process 8 HIP hardware
-    queues when GPU_MAX_HW_QUEUES is unset (so in-flight MSMs overlap without
-    the host setting anything) and leaves a value the process chose alone."""
+def test_library_leaves_process_environment_alone():
+    """Loading the library changes no process-wide HIP setting (the
+    earlier load-time GPU_MAX_HW_QUEUES default depended on load order and
+    reached every other HIP user in the process)."""
     import sys
     code = ("import ctypes, sys; ctypes.CDLL(sys.argv[1]); libc = ctypes.CDLL(None); "
             "libc.getenv.restype = ctypes.c_char_p; print(libc.getenv(b'GPU_MAX_HW_QUEUES'))")
     env = {k: v for k, v in os.environ.items() if k != "GPU_MAX_HW_QUEUES"}
     out = subprocess.run([sys.executable, "-c", code, LIB], env=env, capture_output=True, text=True, check=True)
-    assert out.stdout.strip() == "b'8'"
+    assert out.stdout.strip() == "None"
     env["GPU_MAX_HW_QUEUES"] = "4"
     out = subprocess.run([sys.executable, "-c", code, LIB], env=env, capture_output=True, text=True, check=True)
     assert out.stdout.strip() == "b'4'"

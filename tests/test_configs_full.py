@@ -236,3 +236,61 @@ def test_groth16_2p24_synthetic_pk(gm_ctx, oracle):
             x.free()
     assert got == exp
     _log("sharded world=8 prove matches")
+
+
+@pytest.mark.skipif(os.environ.get("GM_TEST_CONFIG4_FULL") != "1",
+                    reason="opt-in (GM_TEST_CONFIG4_FULL=1): ~8 min of oracle setup + prove on the host cores; "
+                           "run by tools/gpu/config4_full.sh, log in profiles/")
+def test_groth16_2p24_squaring_chain_real_setup(gm_ctx, oracle):
+    """configs[3]'s own circuit (SURVEY.md §8d): groth16_test.go:120-156's
+    refCircuit with 2^24 - 1 squarings (nc = 2^24 constraints, n = 2^24), a real
+    toxic-waste setup by the oracle (setup.go:85-349), a satisfying witness.  The
+    GPU proof -- host inputs, device-resident R1CS with the wires staged in the
+    solver's one-wire levels, plain and precomputed keys -- equals the oracle's
+    byte for byte, and the exponent check accepts it."""
+    import gnark_mi355x as gm
+    cname = "bn254"
+    c = pyref.CURVES[cname]
+    t0 = time.time()
+    r1, W, a, b, cc = R.squaring_chain_fast((1 << 24) - 1, cname, x=3)
+    assert r1.domain_size == 1 << 24 and r1.nc == 1 << 24
+    tox = R.encode_vec(cname, [t % c.r for t in TOXIC])
+    _log("chain 2^24 built (%.0f s); oracle setup" % (time.time() - t0))
+    pk = oracle.g16_setup(cname, r1, tox)
+    rb, sb = R.encode_vec(cname, [0x2424242424]), R.encode_vec(cname, [0x4242424242])
+    _log("oracle setup done (%.0f s); oracle prove" % (time.time() - t0))
+    exp = oracle.g16_prove(cname, pk, r1.nb_public, W, a, b, cc, rb, sb)
+    _log("oracle prove done (%.0f s); exponent check" % (time.time() - t0))
+    assert oracle.g16_check(cname, r1, tox, W, rb, sb, *exp) == 7
+    _log("oracle proof accepted (%.0f s)" % (time.time() - t0))
+    hpk = {k: v for k, v in pk.items() if k != "sizes"}
+    # the resident system: one term per row and matrix, coefficient id 1 (= one) of
+    # gnark's CoeffTable head (0, 1, 2, -1, -2)
+    enc = lambda v: (v * (1 << 256) % c.r).to_bytes(32, "little")
+    table = b"".join(enc(v) for v in (0, 1, 2, c.r - 1, c.r - 2))
+    ones = np.ones(r1.nc, np.uint32)
+    h = gm.R1CS(gm_ctx, cname, r1.nc, r1.nb_wires, r1.rowptr, [ones, ones, ones], r1.wires, table)
+    try:
+        for precompute in (False, True):
+            tu = time.time()
+            dpk = gm.ProvingKey(gm_ctx, cname, hpk, r1.domain_size, r1.nb_wires, r1.nb_public, precompute=precompute)
+            _log("key upload (precompute=%s) %.2f s" % (precompute, time.time() - tu))
+            try:
+                tp = time.time()
+                got = dpk.prove(W, a, b, cc, rb, sb)
+                _log("host-input prove %.1f ms" % ((time.time() - tp) * 1e3))
+                assert got == exp, precompute
+                st = dpk.stage(r1.nc)
+                try:
+                    ns = st.replay_chain(W, 3, r1.nc)  # one wire per solver level, gathered as the Go hook does
+                    got_st = st.prove_r1cs(h, rb, sb)
+                finally:
+                    st.free()
+                _log("staged one-wire levels: %.1f ns per level host side" % ns)
+                assert got_st == exp, precompute
+            finally:
+                dpk.free()
+            _log("gpu proofs (precompute=%s) match the oracle" % precompute)
+    finally:
+        h.free()
+    assert oracle.g16_check(cname, r1, tox, W, rb, sb, *got) == 7

@@ -329,7 +329,14 @@ def test_levelhook_diff_applies_to_the_reference_solver(tmp_path):
     # log entries reach the hook (wires staged during Solve, not after it)
     assert text.count("s.wireLog[n-1-s.nbInputs] = uint32(id)") == 2
     assert text.count("wIDs := solver.wireLog[solver.logMark:end]") == 2
-    assert "st.PutIndexed(gm.StageWires, values, wIDs)" in staged
+    # ... gathered (the squaring chain's one-wire levels cost two appends) and
+    # handed over every stagedFlushAt ids and before the prove
+    assert "run.pendW = append(run.pendW, wIDs...)" in staged
+    assert "run.st.PutIndexed(gm.StageWires, run.values, run.pendW)" in staged
+    assert "run.pendC = append(run.pendC, cIDs...)" in staged
+    pv = staged[staged.index("func (run *stagedRun) prove("):]
+    assert pv.index("run.flushWires()") < pv.index("ProveR1CS") and pv.index("run.flushConstraints()") < pv.index(
+        "ProveR1CS")
     assert "PutRange(gm.StageWires, 0, len(w)" in staged  # only the no-level fallback
     # the diff is what tools/make_levelhook_patch.py generates from the reference
     import importlib.util

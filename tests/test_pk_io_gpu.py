@@ -156,6 +156,42 @@ def test_staged_inputs_by_level(gm_ctx, oracle, cname, k):
         dpk.free()
 
 
+@pytest.mark.parametrize("coalesce,flush_at", [(False, 1), (True, 977), (True, 1 << 16)])
+def test_staged_squaring_chain_level_shape(gm_ctx, oracle, coalesce, flush_at):
+    """The reference benchmark circuit's level shape (groth16_test.go:120-156: a
+    chain of squarings, one constraint and one solved wire per solver level,
+    solver.go:471-484) staged through gm_g16_stage_put_indexed by the C test
+    driver: one put per level and vector, or gathered as the Go level hook does
+    (integration/go/icicle_bn254/staged.go, a put every flush_at ids).  The
+    small puts share ring slots (records gathered in the open slot).  a, b, c
+    and the wires staged -> gm_g16_stage_prove; the wires only with the system
+    resident -> gm_g16_stage_prove_r1cs; both equal the oracle's proof."""
+    import gnark_mi355x as gm
+    k = 3000
+    r1, pk, (W, A, B, C), rb, sb, exp = _setup(oracle, "bn254", k)
+    nc = len(A) // 32
+    assert nc == k + 1 and len(W) // 32 == 3 + k
+    dpk = gm.ProvingKey(gm_ctx, "bn254", pk, r1.domain_size, r1.nb_wires, r1.nb_public)
+    h = gm.R1CS.from_terms(gm_ctx, "bn254", r1.nc, r1.nb_wires, r1.rowptr, r1.wires, r1.coeffs, r1.c.r)
+    try:
+        st = dpk.stage(nc)
+        try:
+            ns = st.replay_chain(W, 3, nc, abc=(A, B, C), coalesce=coalesce, flush_at=flush_at)
+            assert ns > 0
+            assert st.prove(rb, sb) == exp
+        finally:
+            st.free()
+        st = dpk.stage(nc)
+        try:
+            st.replay_chain(W, 3, nc, coalesce=coalesce, flush_at=flush_at)
+            assert st.prove_r1cs(h, rb, sb) == exp
+        finally:
+            st.free()
+    finally:
+        h.free()
+        dpk.free()
+
+
 @pytest.mark.parametrize("reuse", ["1", "0"])
 def test_staged_buffers_reused_across_proofs(gm_ctx, oracle, monkeypatch, reuse):
     """gm_g16_stage_free parks the stage's buffers with the key and the next
