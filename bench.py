@@ -532,6 +532,18 @@ def groth16_bench(ctx, gm, logn, precompute=True, check_oracle=False, staged=Fal
             t_dev.append(time.perf_counter() - t0)
         else:
             t_first = time.perf_counter() - t0  # the key's first prove (its workspace grows)
+    # the same after an idle pause as long as the staged scopes' (a gnark prove
+    # starts after Solve, with the GPU idle): the GPU's way out of idle costs
+    # ~1.3 ms at 2^20 whatever the API (profiles/r06c_staged_overhead.txt)
+    t_dev_idle = []
+    for i in range(reps):
+        for dst, src in zip((A, B, C), srcs):
+            dst.copy_from(src)
+        ctx.synchronize()
+        time.sleep(0.05)
+        t0 = time.perf_counter()
+        dpk.prove_device(W, A, B, C, n, r[:32], r[32:])
+        t_dev_idle.append(time.perf_counter() - t0)
     proof = None
     dpk.prove(host[0], host[1], host[2], host[3], r[:32], r[32:])
     for _ in range(reps):
@@ -572,6 +584,7 @@ def groth16_bench(ctx, gm, logn, precompute=True, check_oracle=False, staged=Fal
     res = {"logn": logn, "pk": "precomputed" if precompute else "plain",
            "roofline": groth16_roofline(n, nb_wires, precompute, med(t_dev)),
            "prove_ms_host_inputs": round(med(t_host) * 1e3, 3), "prove_ms_device_inputs": round(med(t_dev) * 1e3, 3),
+           "prove_ms_device_inputs_after_idle": round(med(t_dev_idle) * 1e3, 3),
            "prove_ms_r1cs_resident": round(med(t_r1cs) * 1e3, 3),
            "prove_ms_r1cs_resident_wires_staged": round(med(t_r1cs_staged) * 1e3, 3),
            "r1cs_staged_matches_r1cs_resident": bool(proof_r1cs_staged == proof_r1cs),
@@ -586,7 +599,8 @@ def groth16_bench(ctx, gm, logn, precompute=True, check_oracle=False, staged=Fal
                     "gm_g16_prove_r1cs); r1cs_resident_wires_staged = the same with the wires staged during "
                     "Solve in one-wire solver levels (gm_g16_stage_prove_r1cs, the Go default path with the "
                     "wire level hook; stage_host_ns_per_level_wires = the Solve-side cost of that staging); all "
-                    "after Solve; pk_upload_s = host arrays to the device key incl. window copies and computeH "
+                    "after Solve; device_inputs_after_idle and the staged scopes start after a 50 ms idle "
+                    "pause (Solve), the other scopes right after GPU work; pk_upload_s = host arrays to the device key incl. window copies and computeH "
                     "tables; first_prove_ms_device_inputs = the key's first prove in this process"}
     if check_oracle or staged:
         res.update(staged_bench(ctx, dpk, n, host, r, proof))

@@ -468,8 +468,13 @@ int gm_msm_async(gm_ctx* ctx, int curve, int g2, const void* scalars_dev, const 
     GM_HIP(hipEventCreateWithFlags(&inputs_read, hipEventDisableTiming));
   }
   {
-    static const bool acc_serial = getenv("GM_MSM_ACC_SERIAL") && atoi(getenv("GM_MSM_ACC_SERIAL")) != 0;
-    ctx->acc_chain = acc_serial && p->st != ctx->stream;  // slot streams only
+    // The in-flight MSMs' accumulations run one after another (gm_ctx::acc_tail):
+    // each launch then runs with the chip's wave slots free of the previous
+    // one, so its start / stop stamps bracket its own execution (the bench's
+    // kernel time; without the order a launch was stamped while it waited for the
+    // previous accumulation's slots).  Same box: 621-624 against 624-630
+    // Mpoints/s unordered (profiles/r06c_acc_chain_ab.txt).
+    ctx->acc_chain = p->st != ctx->stream;  // slot streams only
     StreamSwap sw(ctx, p->st);
     struct ChainOff {
       gm_ctx* c;

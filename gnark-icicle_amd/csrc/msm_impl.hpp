@@ -650,6 +650,7 @@ struct PairSel<Fe2<P, B>> {
     else return k_msm_accum_seg_pair<P, B, false, GM_PAIR_WPE, true>;
   }
   static constexpr auto fixup() { return k_msm_fixup_pair<P, B>; }
+  static constexpr auto fixup_edge() { return k_msm_fixup_edge_pair<P, B>; }
   static constexpr auto fix_tree() { return k_msm_fix_tree_pair<P, B>; }
   static constexpr auto fixup_long() { return k_msm_fixup_long_pair<P, B>; }
   static constexpr auto seg() { return k_msm_seg_pair<P, B>; }
@@ -700,6 +701,40 @@ __global__ void __launch_bounds__(128) k_msm_fixup(const uint32_t* __restrict__ 
   for (uint32_t t = t0 + 1; t <= t1; t++) acc = FullAdd<F>::add(acc, part_first[t]);
   buckets[b] = FullAdd<F>::canon(acc);
 }
+
+// The same merge, one thread per slice edge t >= 1 (GM_FIXUP_EDGE, default): the
+// bucket holding entry t K is cut by the edge when it starts before it, and the
+// thread of its first edge (t = t0 + 1) merges its parts -- the same adds in the
+// same order.  Per bucket, a wave mixes cut and whole buckets and half its lanes
+// idle through the add; per edge, nearly every lane adds (buckets of ~32 entries
+// at K = 64: an edge falls on a bucket boundary with p ~ 1/32).
+template <class F>
+__global__ void __launch_bounds__(128) k_msm_fixup_edge(const uint32_t* __restrict__ keys,
+                                                        const uint32_t* __restrict__ offsets, uint32_t total,
+                                                        uint32_t K, uint32_t nslices,
+                                                        XYZZ<F>* __restrict__ buckets,
+                                                        const XYZZ<F>* __restrict__ part_first,
+                                                        const XYZZ<F>* __restrict__ part_last,
+                                                        uint32_t* __restrict__ maxspan) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x + 1;
+  if (t >= nslices) return;
+  const size_t q = (size_t)t * K;  // first entry of slice t
+  if (q >= offsets[total]) return;
+  const uint32_t b = keys[q];
+  const uint32_t bs = offsets[b];
+  if (bs >= q || bs / K != t - 1) return;  // not cut by this edge, or not its first edge
+  const uint32_t t0 = t - 1, t1 = (offsets[b + 1] - 1) / K;
+  if (t1 - t0 > FIX_SERIAL) {
+    atomicMax(maxspan, t1 - t0);
+    return;
+  }
+  XYZZ<F> acc = part_last[t0];
+  for (uint32_t u = t; u <= t1; u++) acc = FullAdd<F>::add(acc, part_first[u]);
+  buckets[b] = FullAdd<F>::canon(acc);
+}
+#ifndef GM_FIXUP_EDGE
+#define GM_FIXUP_EDGE 1
+#endif
 
 // One level d of the pairwise tree over part_first[t0+1 .. t1] of every long span.
 template <class F>
@@ -1116,7 +1151,8 @@ int msm_launch(gm_ctx* ctx, Arena& arena, const MsmPlan& plan, const void* point
   // 4-7 %, profiles/r04ae_slice_sweep.txt).  Larger MSMs keep 64 (Groth16 2^24:
   // 156.9 vs 159.3 ms at 32).  The long-span bound FIX_SERIAL * K stays above the
   // fullest uniform bucket (64 entries at 2^20).  K % 4 == 0: the accumulation
-  // loads keys / values four entries at a time.
+  // loads keys / values four entries at a time.  (K = 128 for the Groth16 2^24
+  // MSMs: within noise, profiles/r06d_g16_k128_ab.txt.)
   t.K = !G2 && plan.M <= (size_t(1) << 25) ? 32u : 64u;
   int rc;
   constexpr int WORDS = Coord<DF>::WORDS;  // u32 words of one gnark-layout coordinate
@@ -1166,14 +1202,26 @@ int msm_launch(gm_ctx* ctx, Arena& arena, const MsmPlan& plan, const void* point
   }
   {
     ProfScope ps(ctx, "msm_fixup");
-    if constexpr (PairSel<DF>::ok)
+    if (GM_FIXUP_EDGE) {
+      if (nslices > 1) {
+        if constexpr (PairSel<DF>::ok)
+          hipLaunchKernelGGL(PairSel<DF>::fixup_edge(), dim3(blocks_for(2 * (nslices - 1), 128)), dim3(128), 0, st,
+                             plan.keys, plan.offsets, t.total, t.K, (uint32_t)nslices, buckets.as<uint32_t>(),
+                             pfirst.as<uint32_t>(), plast.as<uint32_t>(), errw.as<uint32_t>() + 1, FIX_SERIAL);
+        else
+          hipLaunchKernelGGL(k_msm_fixup_edge<DF>, dim3(blocks_for(nslices - 1, 128)), dim3(128), 0, st, plan.keys,
+                             plan.offsets, t.total, t.K, (uint32_t)nslices, buckets.as<XYZZ<DF>>(),
+                             pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>(), errw.as<uint32_t>() + 1);
+      }
+    } else if constexpr (PairSel<DF>::ok) {
       hipLaunchKernelGGL(PairSel<DF>::fixup(), dim3(blocks_for(2 * (size_t)t.total, 128)), dim3(128), 0, st,
                          plan.offsets, t.total, t.K, buckets.as<uint32_t>(), pfirst.as<uint32_t>(),
                          plast.as<uint32_t>(), errw.as<uint32_t>() + 1, FIX_SERIAL);
-    else
+    } else {
       hipLaunchKernelGGL(k_msm_fixup<DF>, dim3(blocks_for(t.total, 128)), dim3(128), 0, st, plan.offsets, t.total,
                          t.K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(), plast.as<XYZZ<DF>>(),
                          errw.as<uint32_t>() + 1);
+    }
   }
   // Bucket reduction, launched speculatively: buckets spanning more than
   // FIX_SERIAL slices (skewed scalars) are only known once errw[1] (max span)

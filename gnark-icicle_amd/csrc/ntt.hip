@@ -318,10 +318,11 @@ GM_DEV Fe<P> ntt_tw(const Fe<P>* __restrict__ sub, int i) {
 // products of a round: one mad chain each (CH) or the compiler's split columns.
 // A difference that only feeds a product is formed carry-free (fe_sub_cf: value
 // below a + K p with K one above fe_sub_lz's, every product input < 33 p^2 < R' p).
-// NTT_BFLY_CHAIN: the butterflies' chain level (1: one chain per column; the
-// load / store products take CH itself)
+// NTT_BFLY_CHAIN: the butterflies' chain level.  Strict (2, as the load / store
+// products): 2^24 transform 2.072-2.091 -> 2.047-2.061 ms, coset within noise
+// (profiles/r06d_ntt_bfly_chain_ab.txt); 1 = one chain per column (r05).
 #ifndef NTT_BFLY_CHAIN
-#define NTT_BFLY_CHAIN 1
+#define NTT_BFLY_CHAIN 2
 #endif
 #define MUL(x, y) (CH ? fe_mul<P, false, NTT_BFLY_CHAIN>(x, y) : fe_mul_lz(x, y))
 // DIF radix-2 butterfly pair of one round: (u, v) -> (u + v, (u - v + Kp) w)

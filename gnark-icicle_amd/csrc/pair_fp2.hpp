@@ -488,6 +488,33 @@ __global__ void __launch_bounds__(128) k_msm_fixup_pair(const uint32_t* __restri
   pxyzz_store<P>(buckets + (size_t)b * XW, acc);
 }
 
+// k_msm_fixup_edge (msm_impl.hpp) on lane pairs: one pair per slice edge t >= 1
+template <class P, int BETA>
+__global__ void __launch_bounds__(128) k_msm_fixup_edge_pair(const uint32_t* __restrict__ keys,
+                                                             const uint32_t* __restrict__ offsets, uint32_t total,
+                                                             uint32_t K, uint32_t nslices,
+                                                             uint32_t* __restrict__ buckets,
+                                                             const uint32_t* __restrict__ part_first,
+                                                             const uint32_t* __restrict__ part_last,
+                                                             uint32_t* __restrict__ maxspan, uint32_t fix_serial) {
+  constexpr int XW = 8 * P::N;
+  const uint32_t t = ((blockIdx.x * blockDim.x + threadIdx.x) >> 1) + 1;
+  if (t >= nslices) return;
+  const size_t q = (size_t)t * K;
+  if (q >= offsets[total]) return;
+  const uint32_t b = keys[q];
+  const uint32_t bs = offsets[b];
+  if (bs >= q || bs / K != t - 1) return;
+  const uint32_t t0 = t - 1, t1 = (offsets[b + 1] - 1) / K;
+  if (t1 - t0 > fix_serial) {
+    if (!pair_odd()) atomicMax(maxspan, t1 - t0);
+    return;
+  }
+  PXYZZ<P> acc = pxyzz_load<P>(part_last + (size_t)t0 * XW);
+  for (uint32_t u = t; u <= t1; u++) acc = pxyzz_add<P, BETA>(acc, pxyzz_load<P>(part_first + (size_t)u * XW));
+  pxyzz_store<P>(buckets + (size_t)b * XW, acc);
+}
+
 template <class P, int BETA>
 __global__ void __launch_bounds__(128) k_msm_fix_tree_pair(const uint32_t* __restrict__ keys,
                                                            const uint32_t* __restrict__ offsets, uint32_t total,
