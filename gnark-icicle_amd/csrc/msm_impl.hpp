@@ -702,12 +702,16 @@ __global__ void __launch_bounds__(128) k_msm_fixup(const uint32_t* __restrict__ 
   buckets[b] = FullAdd<F>::canon(acc);
 }
 
-// The same merge, one thread per slice edge t >= 1 (GM_FIXUP_EDGE, default): the
-// bucket holding entry t K is cut by the edge when it starts before it, and the
-// thread of its first edge (t = t0 + 1) merges its parts -- the same adds in the
-// same order.  Per bucket, a wave mixes cut and whole buckets and half its lanes
-// idle through the add; per edge, nearly every lane adds (buckets of ~32 entries
-// at K = 64: an edge falls on a bucket boundary with p ~ 1/32).
+// The same merge, one thread per slice edge t >= 1: the bucket holding entry t K
+// is cut by the edge when it starts before it, and the thread of its first edge
+// (t = t0 + 1) merges its parts -- the same adds in the same order.  Used when
+// buckets are shorter than a slice (M < K * buckets: the plain-key Groth16 2^24
+// MSMs, ~32 entries per bucket at K = 64): per bucket, a wave then mixes cut and
+// whole buckets and half its lanes idle through the add, while nearly every
+// edge cuts a bucket once.  Buckets longer than a slice are cut by one to three
+// edges each, so per edge the lanes idle instead: 2^24 plain 148.2 -> 147.3 ms,
+// precomputed (~96 entries per bucket) 137.5 -> 140.8 ms, 2^20 G1 (64 per bucket
+// at K = 32) fixup 0.11 -> 0.175 ms (profiles/r06g_fixup_edge_ab.txt).
 template <class F>
 __global__ void __launch_bounds__(128) k_msm_fixup_edge(const uint32_t* __restrict__ keys,
                                                         const uint32_t* __restrict__ offsets, uint32_t total,
@@ -732,10 +736,6 @@ __global__ void __launch_bounds__(128) k_msm_fixup_edge(const uint32_t* __restri
   for (uint32_t u = t; u <= t1; u++) acc = FullAdd<F>::add(acc, part_first[u]);
   buckets[b] = FullAdd<F>::canon(acc);
 }
-#ifndef GM_FIXUP_EDGE
-#define GM_FIXUP_EDGE 1
-#endif
-
 // One level d of the pairwise tree over part_first[t0+1 .. t1] of every long span.
 template <class F>
 __global__ void __launch_bounds__(128) k_msm_fix_tree(const uint32_t* __restrict__ keys,
@@ -1202,7 +1202,7 @@ int msm_launch(gm_ctx* ctx, Arena& arena, const MsmPlan& plan, const void* point
   }
   {
     ProfScope ps(ctx, "msm_fixup");
-    if (GM_FIXUP_EDGE) {
+    if (plan.M < (size_t)t.K * t.total) {  // buckets shorter than a slice: per edge
       if (nslices > 1) {
         if constexpr (PairSel<DF>::ok)
           hipLaunchKernelGGL(PairSel<DF>::fixup_edge(), dim3(blocks_for(2 * (nslices - 1), 128)), dim3(128), 0, st,
