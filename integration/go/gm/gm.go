@@ -50,15 +50,20 @@ const PkPrecompute = C.GM_PK_PRECOMPUTE
 const PkPrecomputeAuto = C.GM_PK_PRECOMPUTE_AUTO
 
 // PrecomputeFlags maps GNARK_MI355X_PRECOMPUTE to upload flags: "1" always,
-// "0" never, unset or "auto" when the copies fit (PkPrecomputeAuto).
+// "auto" when the copies fit (PkPrecomputeAuto), unset or "0" never.  The
+// copies pay off only for a key that proves many times: at 2^24 (BN254, one
+// MI355X) they add 4.3 s to the upload and save 9.8 ms per proof, break-even
+// ~440 proofs; at 2^20 0.28 s against 1.3 ms, ~220 proofs (bench.py
+// precompute_break_even, profiles/r06e_bench.json).  A process that proves once
+// reaches its first proof in 3.1 s plain against 7.1 s precomputed.
 func PrecomputeFlags() uint {
 	switch os.Getenv("GNARK_MI355X_PRECOMPUTE") {
 	case "1":
 		return PkPrecompute
-	case "0":
-		return 0
-	default:
+	case "auto":
 		return PkPrecomputeAuto
+	default:
+		return 0
 	}
 }
 

@@ -66,9 +66,10 @@ func kWires(r1cs *cs.R1CS, nbWires int) []uint32 {
 }
 
 // setupDevicePointers uploads the key once (icicle.go:31-130).  The point arrays
-// are converted to the MSM layout on the device; by default the key also keeps
-// fixed-base window copies when they fit the device (~12x the point memory,
-// -14% prove time at 2^24; GNARK_MI355X_PRECOMPUTE=0 / 1 forces them off / on).
+// are converted to the MSM layout on the device.  GNARK_MI355X_PRECOMPUTE=1 /
+// auto also keeps fixed-base window copies (always / when they fit the device:
+// ~12x the point memory, -7% prove time at 2^24, +4.3 s of upload, so they pay
+// off after ~440 proofs of one key; gm.PrecomputeFlags).
 func (pk *ProvingKey) setupDevicePointers(r1cs *cs.R1CS) error {
 	if pk.deviceInfo != nil {
 		return nil
@@ -95,7 +96,7 @@ func (pk *ProvingKey) setupDevicePointers(r1cs *cs.R1CS) error {
 	if len(pk.G2.B) > 0 {
 		k.B2 = unsafe.Pointer(&pk.G2.B[0])
 	}
-	flags := gm.PrecomputeFlags() // default: window copies when they fit the device
+	flags := gm.PrecomputeFlags() // default: no window copies (gm.PrecomputeFlags)
 	key, err := gm.UploadG16Key(gm.BN254, k, flags)
 	if err != nil {
 		return err

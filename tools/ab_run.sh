@@ -2,8 +2,8 @@
 # Same-box A/B runner (the pattern behind the profiles/r0*_ab.txt files): runs COMMAND once per
 # environment variant, alternating variants in fresh processes for REPS rounds, each run under its own
 # time limit, and appends "variant | output" lines to OUT.  Stops at the first failing run.
-#   bash tools/ab_run.sh OUT REPS "GM_X=0" "GM_X=1" -- python3 tools/msm_only.py --logn 20 --reps 5
-#   bash tools/ab_run.sh gpurun_out/ab.txt 2 "" "GM_G16_H_INCREMENTAL=0" -- python3 tools/g16_host_trace.py devonly
+#   bash tools/ab_run.sh OUT REPS "" "GNARK_MI355X_LIB=$PWD/gnark-icicle_amd/libgnark_mi355x_alt.so" -- python3 tools/msm_only.py
+# (the variant is an alternative build of the library, or any environment the command reads)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=$1; REPS=$2; shift 2
