@@ -318,7 +318,7 @@ class Context:
         _check(load_library().gm_set_msm_window(self.handle, c))
 
     def set_msm_glv(self, mode: int):
-        """GLV split of plain MSMs: 1 on, 0 off, -1 environment default."""
+        """GLV split of plain MSMs: 1 on, 0 off, -1 the size rule (on up to 2^21 points)."""
         _check(load_library().gm_set_msm_glv(self.handle, mode))
 
     # ---- MSM -----------------------------------------------------------------

@@ -1,0 +1,20 @@
+#!/bin/bash
+# r06p: four MSM slots (GM_MSM_SLOTS=4 build) with the bench pipelined 4 deep, with and without the separate
+# (experiment not kept: its code is not in the tree; the script documents how profiles/r06p_*.txt was measured)
+# accumulation stream (r06o), vs three slots / 3 deep (default)
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out && export TMPDIR=/tmp
+L=$PWD/gnark-icicle_amd
+GNARK_MI355X_LIB=$L/libgnark_mi355x_s4.so timeout -k 10 300 python -u -m pytest tests/test_msm_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -k "(async or bench or uniform) and not async_pipelined" > gpurun_out/r06p_tests.log 2>&1 || { tail -30 gpurun_out/r06p_tests.log; exit 1; }
+tail -1 gpurun_out/r06p_tests.log
+AB_TIMEOUT=150 bash tools/ab_run.sh gpurun_out/r06p_ab.txt 4 "" "GNARK_MI355X_LIB=$L/libgnark_mi355x_s4.so GM_BENCH_PIPE_DEPTH=4" "GNARK_MI355X_LIB=$L/libgnark_mi355x_s4a1.so GM_BENCH_PIPE_DEPTH=4" -- python3 bench.py --steps 30 --warmup 5 --no-secondary --no-cpu-baseline > /dev/null || exit 1
+python3 - <<'PY'
+import json
+for l in open("gpurun_out/r06p_ab.txt"):
+    tag, js = l.split(" | ", 1)
+    d = json.loads(js); r = d["roofline"]
+    print(tag.replace("/root/repo/gnark-icicle_amd/", ""), d["value"], d["ms_per_step"], r["avg_launch_ms"], r.get("timing_source"), d["latency_ms"])
+PY
+GNARK_MI355X_LIB=$L/libgnark_mi355x_s4.so GM_BENCH_PIPE_DEPTH=4 timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r06p_kt -o kt -- python3 bench.py --steps 20 --warmup 5 --no-secondary --no-cpu-baseline > gpurun_out/r06p_kt.json 2> gpurun_out/r06p_kt.err || { tail -20 gpurun_out/r06p_kt.err; exit 1; }
+gzip -f $(find gpurun_out/r06p_kt -name "*kernel_trace.csv")

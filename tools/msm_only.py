@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--window", type=int, default=0)
     ap.add_argument("--scalars", default="uniform")
     ap.add_argument("--precompute", action="store_true")
+    ap.add_argument("--glv", type=int, default=-1, help="gm_set_msm_glv mode (-1 = the size rule)")
     a = ap.parse_args()
     import numpy as np
     import gnark_mi355x as gm
@@ -46,6 +47,7 @@ def main():
         P = ctx.batch_mul_base(a.curve, a.g2, gm.generator(a.curve, a.g2), K, n)
         K.free()
         ctx.set_msm_window(a.window)
+        ctx.set_msm_glv(a.glv)
         if a.precompute:
             pre = ctx.points_upload_precomputed(a.curve, P.to_host(), a.g2, 0)
             run = lambda: ctx.msm_precomputed(a.curve, S, pre, n, g2=a.g2)
@@ -61,8 +63,8 @@ def main():
         dt = (time.perf_counter() - t0) / a.reps
         st = ctx.profile_stats()
         ks = " ".join("%s=%.4f" % (k, v[0] / max(v[1], 1)) for k, v in sorted(st.items()))
-        print("%s %s 2^%d %s window=%d: %.4f ms/MSM  %.1f Mpoints/s | %s" % (
-            a.curve, "g2" if a.g2 else "g1", a.logn, a.scalars, a.window, dt * 1e3, n / dt / 1e6, ks), flush=True)
+        print("%s %s 2^%d %s window=%d glv=%d: %.4f ms/MSM  %.1f Mpoints/s | %s" % (
+            a.curve, "g2" if a.g2 else "g1", a.logn, a.scalars, a.window, a.glv, dt * 1e3, n / dt / 1e6, ks), flush=True)
 
 
 if __name__ == "__main__":
