@@ -789,17 +789,26 @@ __global__ void __launch_bounds__(128) k_msm_fixup_long(const uint32_t* __restri
 // block with one task per thread measured no faster at 2^20: the tree's tail
 // is short of blocks, not of threads.)
 constexpr uint32_t BS_THREADS = 256;
+// A bucket with no entries (offsets[b] == offsets[b + 1]) was never written by
+// the accumulation or the fixup: it reads as infinity here, so the buckets need no
+// clearing before the accumulation (a 1 GB memset per plain 2^24 MSM).
 template <class F>
-__global__ void __launch_bounds__(128) k_msm_seg(const XYZZ<F>* __restrict__ buckets, uint32_t nb,
-                                                 uint32_t L, uint32_t nseg, uint32_t W,
-                                                 XYZZ<F>* __restrict__ nodes) {
+__global__ void __launch_bounds__(128) k_msm_seg(const XYZZ<F>* __restrict__ buckets,
+                                                 const uint32_t* __restrict__ offsets, uint32_t nb, uint32_t L,
+                                                 uint32_t nseg, uint32_t W, XYZZ<F>* __restrict__ nodes) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= W * nseg) return;
   const uint32_t w = t / nseg, s = t % nseg;
-  const XYZZ<F>* B = buckets + (size_t)w * nb + (size_t)s * L;
-  XYZZ<F> S = B[L - 1], T = S;
+  const size_t b0 = (size_t)w * nb + (size_t)s * L;
+  const XYZZ<F>* B = buckets + b0;
+  const uint32_t* O = offsets + b0;
+  uint32_t o_hi = O[L];
+  uint32_t o_lo = O[L - 1];
+  XYZZ<F> S = o_lo == o_hi ? xyzz_inf<F>() : B[L - 1], T = S;
   for (int j = (int)L - 2; j >= 0; j--) {
-    S = FullAdd<F>::add(S, B[j]);
+    o_hi = o_lo;
+    o_lo = O[j];
+    S = FullAdd<F>::add(S, o_lo == o_hi ? xyzz_inf<F>() : B[j]);
     T = FullAdd<F>::add(T, S);
   }
   nodes[2 * (size_t)t] = FullAdd<F>::canon(S);
@@ -1025,12 +1034,14 @@ int msm_reduce(gm_ctx* ctx, MsmTail& t) {
   if constexpr (PairSel<DF>::ok) {
     if (pairs)
       hipLaunchKernelGGL(PairSel<DF>::seg(), dim3(blocks_for(2 * (size_t)t.Wr * t.nseg, 128)), dim3(128), 0, st,
-                         (const uint32_t*)t.buckets, t.nb, t.L, t.nseg, t.Wr, (uint32_t*)t.nodes_a);
+                         (const uint32_t*)t.buckets, (const uint32_t*)t.offsets, t.nb, t.L, t.nseg, t.Wr,
+                         (uint32_t*)t.nodes_a);
   }
   if constexpr (kOneLane<DF>) {
     if (!pairs)
       hipLaunchKernelGGL(k_msm_seg<DF>, dim3(blocks_for((size_t)t.Wr * t.nseg, 128)), dim3(128), 0, st,
-                         (const XYZZ<DF>*)t.buckets, t.nb, t.L, t.nseg, t.Wr, (XYZZ<DF>*)t.nodes_a);
+                         (const XYZZ<DF>*)t.buckets, (const uint32_t*)t.offsets, t.nb, t.L, t.nseg, t.Wr,
+                         (XYZZ<DF>*)t.nodes_a);
   }
   // LDS tree levels until one node per window
   constexpr size_t SLOT_BUDGET = (96u << 10) / sizeof(XYZZ<DF>);
@@ -1174,7 +1185,6 @@ int msm_launch(gm_ctx* ctx, Arena& arena, const MsmPlan& plan, const void* point
   t.plast = plast.p;
   GM_HIP(hipMemsetAsync(errw.p, 0, 16, st));
   {
-    GM_HIP(hipMemsetAsync(buckets.p, 0, sizeof(XYZZ<DF>) * (size_t)t.total, st));  // all-zero XYZZ = infinity
     // async MSMs: this accumulation starts after the previous one (gm_ctx::acc_tail)
     if (ctx->acc_chain) {
       if (!ctx->acc_tail) GM_HIP(hipEventCreateWithFlags(&ctx->acc_tail, hipEventDisableTiming));

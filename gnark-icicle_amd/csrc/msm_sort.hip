@@ -376,20 +376,29 @@ static __global__ void __launch_bounds__(1024) k_msm_s2_local(const uint64_t* __
   }
 }
 
-static __global__ void __launch_bounds__(1024) k_msm_s2_scan(const uint32_t* __restrict__ cbase, uint32_t F,
-                                                             uint32_t T, uint32_t* __restrict__ fcount,
+// The split-bin kernels below run on a capped grid, block-strided over the bins /
+// parts: with no split bin (uniform digits) every block returns at once, where a
+// block per bin cost ~0.2 ms per launch at 2^24 (213K empty blocks).
+constexpr uint32_t S2_SPLIT_GRID = 2048;
+static __global__ void __launch_bounds__(1024) k_msm_s2_scan(const uint32_t* __restrict__ cbase,
+                                                             const uint32_t* __restrict__ pbase, uint32_t NC,
+                                                             uint32_t F, uint32_t T, uint32_t* __restrict__ fcount,
                                                              uint32_t* __restrict__ offsets) {
   extern __shared__ uint32_t hist[];
   __shared__ uint32_t wsum[17];
-  const uint32_t H = blockIdx.x, t = threadIdx.x;
-  const uint32_t start = cbase[H], cnt = cbase[H + 1] - start;
-  if (cnt <= S2_BIG) return;
-  const uint32_t b0 = H << F, nf = min(1u << F, T - b0);
-  for (uint32_t f = t; f < nf; f += S_THREADS) hist[f] = fcount[b0 + f];
-  block_excl_scan(hist, nf, wsum);
-  for (uint32_t f = t; f < nf; f += S_THREADS) {
-    offsets[b0 + f] = start + hist[f];
-    fcount[b0 + f] = start + hist[f];  // now the bucket's write cursor
+  if (pbase[NC] == NC) return;  // no split bins
+  const uint32_t t = threadIdx.x;
+  for (uint32_t H = blockIdx.x; H < NC; H += gridDim.x) {
+    const uint32_t start = cbase[H], cnt = cbase[H + 1] - start;
+    if (cnt <= S2_BIG) continue;
+    const uint32_t b0 = H << F, nf = min(1u << F, T - b0);
+    for (uint32_t f = t; f < nf; f += S_THREADS) hist[f] = fcount[b0 + f];
+    block_excl_scan(hist, nf, wsum);
+    for (uint32_t f = t; f < nf; f += S_THREADS) {
+      offsets[b0 + f] = start + hist[f];
+      fcount[b0 + f] = start + hist[f];  // now the bucket's write cursor
+    }
+    __syncthreads();
   }
 }
 
@@ -402,29 +411,33 @@ static __global__ void __launch_bounds__(1024) k_msm_s2_scatter(const uint64_t* 
                                                                 uint32_t* __restrict__ vals_out) {
   extern __shared__ uint32_t s2_lds[];
   __shared__ uint32_t sh[2];
-  const uint32_t j = blockIdx.x, t = threadIdx.x;
-  if (j >= pbase[NC] || pbase[NC] == NC) return;  // no split bins: nothing to do
-  s2_locate(pbase, NC, j, sh);
-  const uint32_t H = sh[0], p = sh[1];
-  const uint32_t start = cbase[H], cnt = cbase[H + 1] - start;
-  if (cnt <= S2_BIG) return;
-  const uint32_t b0 = H << F, nf = min(1u << F, T - b0), fmask = (1u << F) - 1;
-  uint32_t* hist = s2_lds;
-  uint32_t* cur = s2_lds + nf;
-  for (uint32_t q = t; q < nf; q += S_THREADS) hist[q] = 0;
-  __syncthreads();
-  const uint32_t lo = p * S2_BIG, hi = min(lo + S2_BIG, cnt);
-  for (uint32_t e = lo + t; e < hi; e += S_THREADS) lds_rank_add(hist, (uint32_t)tmp[start + e] & fmask);
-  __syncthreads();
-  for (uint32_t f = t; f < nf; f += S_THREADS)
-    if (hist[f]) cur[f] = atomicAdd(&fcursor[b0 + f], hist[f]);
-  __syncthreads();
-  for (uint32_t e = lo + t; e < hi; e += S_THREADS) {
-    const uint64_t x = tmp[start + e];
-    const uint32_t b = (uint32_t)x;
-    const uint32_t pos = lds_rank_add(cur, b & fmask);
-    keys_out[pos] = b;
-    vals_out[pos] = (uint32_t)(x >> 32);
+  const uint32_t t = threadIdx.x, parts = pbase[NC];
+  if (parts == NC) return;  // no split bins: nothing to do
+  for (uint32_t j = blockIdx.x; j < parts; j += gridDim.x) {
+    s2_locate(pbase, NC, j, sh);
+    const uint32_t H = sh[0], p = sh[1];
+    const uint32_t start = cbase[H], cnt = cbase[H + 1] - start;
+    __syncthreads();  // every thread has read sh before the next part's s2_locate
+    if (cnt <= S2_BIG) continue;
+    const uint32_t b0 = H << F, nf = min(1u << F, T - b0), fmask = (1u << F) - 1;
+    uint32_t* hist = s2_lds;
+    uint32_t* cur = s2_lds + nf;
+    for (uint32_t q = t; q < nf; q += S_THREADS) hist[q] = 0;
+    __syncthreads();
+    const uint32_t lo = p * S2_BIG, hi = min(lo + S2_BIG, cnt);
+    for (uint32_t e = lo + t; e < hi; e += S_THREADS) lds_rank_add(hist, (uint32_t)tmp[start + e] & fmask);
+    __syncthreads();
+    for (uint32_t f = t; f < nf; f += S_THREADS)
+      if (hist[f]) cur[f] = atomicAdd(&fcursor[b0 + f], hist[f]);
+    __syncthreads();
+    for (uint32_t e = lo + t; e < hi; e += S_THREADS) {
+      const uint64_t x = tmp[start + e];
+      const uint32_t b = (uint32_t)x;
+      const uint32_t pos = lds_rank_add(cur, b & fmask);
+      keys_out[pos] = b;
+      vals_out[pos] = (uint32_t)(x >> 32);
+    }
+    __syncthreads();  // the LDS is reused by the next part
   }
 }
 
@@ -502,10 +515,11 @@ int msm_sort_digits(gm_ctx* ctx, Arena& arena, const SortGeom& g, size_t n, uint
   hipLaunchKernelGGL(k_msm_s2_local, dim3((unsigned)maxparts), dim3(S_THREADS),
                      sizeof(uint32_t) * (nfmax + 2 * S2_STAGE), st, fin, cbase, pbase, g.NC, g.F, g.T,
                      fcount.as<uint32_t>(), keys_out, vals_out, offsets);
-  hipLaunchKernelGGL(k_msm_s2_scan, dim3(g.NC), dim3(S_THREADS), sizeof(uint32_t) * nfmax, st, cbase, g.F, g.T,
-                     fcount.as<uint32_t>(), offsets);
-  hipLaunchKernelGGL(k_msm_s2_scatter, dim3((unsigned)maxparts), dim3(S_THREADS), 2 * sizeof(uint32_t) * nfmax, st,
-                     fin, cbase, pbase, g.NC, g.F, g.T, fcount.as<uint32_t>(), keys_out, vals_out);
+  hipLaunchKernelGGL(k_msm_s2_scan, dim3(std::min<uint32_t>(g.NC, S2_SPLIT_GRID)), dim3(S_THREADS),
+                     sizeof(uint32_t) * nfmax, st, cbase, pbase, g.NC, g.F, g.T, fcount.as<uint32_t>(), offsets);
+  hipLaunchKernelGGL(k_msm_s2_scatter, dim3((unsigned)std::min<size_t>(maxparts, S2_SPLIT_GRID)), dim3(S_THREADS),
+                     2 * sizeof(uint32_t) * nfmax, st, fin, cbase, pbase, g.NC, g.F, g.T, fcount.as<uint32_t>(),
+                     keys_out, vals_out);
   GM_HIP(hipGetLastError());
   return GM_OK;
 }

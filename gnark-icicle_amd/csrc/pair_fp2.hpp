@@ -552,17 +552,25 @@ __global__ void __launch_bounds__(128) k_msm_fixup_long_pair(const uint32_t* __r
   pxyzz_store<P>(buckets + (size_t)b * XW, r);
 }
 
+// (empty buckets read as infinity, as in k_msm_seg)
 template <class P, int BETA>
-__global__ void __launch_bounds__(128) k_msm_seg_pair(const uint32_t* __restrict__ buckets, uint32_t nb, uint32_t L,
+__global__ void __launch_bounds__(128) k_msm_seg_pair(const uint32_t* __restrict__ buckets,
+                                                      const uint32_t* __restrict__ offsets, uint32_t nb, uint32_t L,
                                                       uint32_t nseg, uint32_t W, uint32_t* __restrict__ nodes) {
   constexpr int XW = 8 * P::N;
   const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
   if (t >= W * nseg) return;
   const uint32_t w = t / nseg, s = t % nseg;
-  const uint32_t* B = buckets + ((size_t)w * nb + (size_t)s * L) * XW;
-  PXYZZ<P> S = pxyzz_load<P>(B + (size_t)(L - 1) * XW), T = S;
+  const size_t b0 = (size_t)w * nb + (size_t)s * L;
+  const uint32_t* B = buckets + b0 * XW;
+  const uint32_t* O = offsets + b0;
+  uint32_t o_hi = O[L];
+  uint32_t o_lo = O[L - 1];
+  PXYZZ<P> S = o_lo == o_hi ? pxyzz_inf<P>() : pxyzz_load<P>(B + (size_t)(L - 1) * XW), T = S;
   for (int j = (int)L - 2; j >= 0; j--) {
-    S = pxyzz_add<P, BETA>(S, pxyzz_load<P>(B + (size_t)j * XW));
+    o_hi = o_lo;
+    o_lo = O[j];
+    S = pxyzz_add<P, BETA>(S, o_lo == o_hi ? pxyzz_inf<P>() : pxyzz_load<P>(B + (size_t)j * XW));
     T = pxyzz_add<P, BETA>(T, S);
   }
   pxyzz_store<P>(nodes + 2 * (size_t)t * XW, S);
