@@ -954,7 +954,11 @@ int msm_plan(gm_ctx* ctx, Arena& arena, const void* scalars_dev, size_t n, const
   // A GLV plan's windows are full width (|k1|, |k2| < 0.87 * 2^127: no narrow top
   // window) with twice the entries per bucket: ~4K-entry bins keep one pass-1
   // block within 512 bins (no middle pass) and still fit S2_STAGE.
-  const double bin_entries = glv ? 4096.0 : 2048.0;
+  // The shared-bucket (precomputed) layout takes ~1.5K-entry bins: its 2^24 sort 3.78 -> 3.34 ms, 2^20 0.28 ->
+  // 0.19 ms against ~0.75K, while ~3K are slower again (profiles/r06v_shared_sort_bins_ab.txt); the plain
+  // layout's 2^24 sort is slower with ~2K bins than ~1K (3.29 -> 3.51 ms, r06u_sort_bins_ab.txt) and with ~0.5K
+  // (3.35 -> 3.83 ms, r06w_plain_sort_bins_ab.txt).
+  const double bin_entries = glv || shared ? 4096.0 : 2048.0;
   while (sg.F < 13 && (double)M * std::ldexp(1.0, (int)sg.F + 1) <= bin_entries * sg.T) sg.F++;
   auto bins = [&](uint32_t sh) { return (uint32_t)(((uint64_t)sg.T + (1ull << sh) - 1) >> sh); };
   auto touched = [&](uint32_t sh) { return shared ? bins(sh) : std::max(1u, plan.nb >> sh); };
