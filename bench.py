@@ -188,7 +188,14 @@ def main():
         step()
     lat_ms = (time.perf_counter() - t0) / 3 * 1e3
     ctx.profile(False)
-    iso_ms, iso_cnt = ctx.profile_stats().get("msm_accum_g1", (0.0, 0))
+    # the accumulation's own execution: first wave start .. last wave end, stamped by
+    # its waves (msm_accum_g1_exec, csrc/runtime.hpp ProfScope::wave_stamp); the
+    # launch's event brackets (msm_accum_g1) also hold the time it waited for wave
+    # slots held by the other MSMs' kernels
+    iso_stats = ctx.profile_stats()
+    iso_ms, iso_cnt = iso_stats.get("msm_accum_g1_exec", (0.0, 0))
+    if not iso_cnt:
+        iso_ms, iso_cnt = iso_stats.get("msm_accum_g1", (0.0, 0))
     iso_avg_ms = iso_ms / max(iso_cnt, 1)
     ctx.profile_reset()
     ctx.profile(True)
@@ -208,7 +215,12 @@ def main():
     value = total_points / (dt / args.steps) / 1e6
 
     # ---- roofline of the dominant kernel (bucket accumulation) ------------------
-    acc_ms, acc_cnt = stats.get("msm_accum_g1", (0.0, 0))
+    br_ms, br_cnt = stats.get("msm_accum_g1", (0.0, 0))
+    bracket_avg_ms = br_ms / max(br_cnt, 1)
+    acc_ms, acc_cnt = stats.get("msm_accum_g1_exec", (0.0, 0))
+    stamped = acc_cnt > 0
+    if not stamped:
+        acc_ms, acc_cnt = br_ms, br_cnt
     acc_avg_ms = acc_ms / max(acc_cnt, 1)
     # A launch time above the step time cannot be the kernel's own run time (the
     # launches would overlap each other): such a figure is not a kernel time and
@@ -241,13 +253,17 @@ def main():
                           "traffic_streaming_corrected = 2 x FETCH + WRITE (the guide's streaming factor); committed "
                           "profile of this kernel, not measured in this run)",
         "avg_launch_ms": round(acc_avg_ms, 4),
-        "timing": ("hipExtLaunchKernelGGL start / stop events of every accumulation launch in the timed loop "
-                   "(csrc/msm_impl.hpp); the in-flight MSMs' accumulations run one after another "
-                   "(gm_ctx::acc_tail), so each bracket is one kernel's own run, beside the other MSMs' sorts "
-                   "and reductions" if pipelined_ok else
+        "timing": (("wave stamps of every accumulation launch in the timed loop: the wall clock of its first "
+                    "wave's start and last wave's end (csrc/msm_impl.hpp wave_stamp_begin / _end), i.e. the "
+                    "kernel's own execution beside the other MSMs' sorts and reductions; the in-flight MSMs' "
+                    "accumulations run one after another (gm_ctx::acc_tail).  The launches' "
+                    "hipExtLaunchKernelGGL event brackets average %.4f ms: they also hold the time a launch waited "
+                    "for wave slots" % bracket_avg_ms) if pipelined_ok and stamped else
+                   ("hipExtLaunchKernelGGL start / stop events of every accumulation launch in the timed loop "
+                    "(csrc/msm_impl.hpp)") if pipelined_ok else
                    "the timed loop's launch average (%.4f ms) exceeds ms_per_step, so it is not a kernel time: "
                    "avg_launch_ms / achieved / frac are the isolated launch's (below)" % pipelined_avg_ms),
-        "timing_source": "pipelined" if pipelined_ok else "isolated",
+        "timing_source": ("pipelined_wave_stamps" if stamped else "pipelined") if pipelined_ok else "isolated",
         "bytes_per_launch": alg_bytes,
         "int_alu": {"achieved": round(tmads, 3), "peak": round(MAD_PEAK_T, 2), "unit": "T v_mad_u64_u32/s",
                     "frac": round(tmads / MAD_PEAK_T, 4),

@@ -184,6 +184,7 @@ int gm_destroy(gm_ctx* ctx) {
     if (s) hipStreamDestroy(s);
   if (ctx->g16_stream) hipStreamDestroy(ctx->g16_stream);
   if (ctx->acc_tail) hipEventDestroy(ctx->acc_tail);
+  if (ctx->stamp_dev) hipFree(ctx->stamp_dev);
   hipStreamDestroy(ctx->stream);
   if (ctx->aux) hipStreamDestroy(ctx->aux);
   if (ctx->copy) hipStreamDestroy(ctx->copy);
@@ -247,6 +248,7 @@ int gm_profile_reset(gm_ctx* ctx) {
   gm::CtxLock g(ctx);
   hipStreamSynchronize(ctx->stream);
   prof_collect(ctx);
+  stamp_collect(ctx);
   ctx->stats.clear();
   return GM_OK;
 }
@@ -254,6 +256,7 @@ int gm_profile_get(gm_ctx* ctx, const char* name, double* total_ms, uint64_t* co
   gm::CtxLock g(ctx);
   hipStreamSynchronize(ctx->stream);
   prof_collect(ctx);
+  stamp_collect(ctx);
   auto it = ctx->stats.find(name);
   if (it == ctx->stats.end()) {
     *total_ms = 0;
@@ -268,6 +271,7 @@ int gm_profile_dump(gm_ctx* ctx, char* buf, size_t cap) {
   gm::CtxLock g(ctx);
   hipStreamSynchronize(ctx->stream);
   prof_collect(ctx);
+  stamp_collect(ctx);
   std::string s;
   for (auto& kv : ctx->stats)
     s += kv.first + " " + std::to_string(kv.second.total_ms) + " " + std::to_string(kv.second.count) + "\n";

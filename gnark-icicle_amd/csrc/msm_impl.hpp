@@ -514,6 +514,16 @@ GM_DEV void accum_emit(uint32_t b, const XYZZ<F>& acc_raw, bool is_first, bool i
   }
 }
 
+// Profiled launches (ProfScope::wave_stamp): lane 0 of every wave stamps the wall
+// clock on entry (atomicMin) and after the body, where the wave's lanes have
+// reconverged (atomicMax): first wave start .. last wave end of the launch.
+GM_DEV void wave_stamp_begin(unsigned long long* stamp) {
+  if (stamp && (threadIdx.x & 63) == 0) atomicMin(stamp, (unsigned long long)wall_clock64());
+}
+GM_DEV void wave_stamp_end(unsigned long long* stamp) {
+  if (stamp && (threadIdx.x & 63) == 0) atomicMax(stamp + 1, (unsigned long long)wall_clock64());
+}
+
 // G1 accumulation body: keys and values arrive four entries per 16-byte load
 // instead of one 4-byte load per entry (r05).  A thread's slice is K
 // consecutive entries and consecutive lanes are K entries apart, so each 4-byte
@@ -596,8 +606,11 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4)))
 k_msm_accum_seg_ch(const uint32_t* __restrict__ points, uint32_t n, const uint32_t* __restrict__ keys,
                    const uint32_t* __restrict__ vals, const uint32_t* __restrict__ offsets, uint32_t total,
                    uint32_t K, XYZZ<F>* __restrict__ buckets, XYZZ<F>* __restrict__ part_first,
-                   XYZZ<F>* __restrict__ part_last, uint32_t* __restrict__ err) {
+                   XYZZ<F>* __restrict__ part_last, uint32_t* __restrict__ err,
+                   unsigned long long* __restrict__ stamp) {
+  wave_stamp_begin(stamp);
   accum_seg_body_v4<F, true>(points, n, keys, vals, offsets, total, K, buckets, part_first, part_last, err);
+  wave_stamp_end(stamp);
 }
 // Four waves fit the 9-limb fields only: BLS12-377's 14-limb add spills 216
 // VGPRs under the cap and takes the prefetching kernel (two waves, no spill).
@@ -619,8 +632,11 @@ __global__ void __launch_bounds__(128) k_msm_accum_seg_pf4(const uint32_t* __res
                                                            uint32_t K, XYZZ<F>* __restrict__ buckets,
                                                            XYZZ<F>* __restrict__ part_first,
                                                            XYZZ<F>* __restrict__ part_last,
-                                                           uint32_t* __restrict__ err) {
+                                                           uint32_t* __restrict__ err,
+                                                           unsigned long long* __restrict__ stamp) {
+  wave_stamp_begin(stamp);
   accum_seg_body_v4<F, false, true>(points, n, keys, vals, offsets, total, K, buckets, part_first, part_last, err);
+  wave_stamp_end(stamp);
 }
 // G1 accumulation kernel of a field
 template <class F>
@@ -1211,7 +1227,7 @@ int msm_launch(gm_ctx* ctx, Arena& arena, const MsmPlan& plan, const void* point
       hipExtLaunchKernelGGL(g1_accum_kernel<DF>(), dim3(blocks_for(nslices, 128)), dim3(128), 0, st, ps.a, ps.b, 0,
                             reinterpret_cast<const uint32_t*>(points_internal), (uint32_t)plan.npts, plan.keys,
                             plan.vals, plan.offsets, t.total, t.K, buckets.as<XYZZ<DF>>(), pfirst.as<XYZZ<DF>>(),
-                            plast.as<XYZZ<DF>>(), errw.as<uint32_t>());
+                            plast.as<XYZZ<DF>>(), errw.as<uint32_t>(), ps.wave_stamp("msm_accum_g1_exec"));
     }
   }
   {

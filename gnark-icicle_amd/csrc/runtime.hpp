@@ -67,6 +67,15 @@ struct gm_ctx {
   std::vector<Pending> pending;
   std::vector<hipEvent_t> event_pool;
   std::map<std::string, gm::KernelStat> stats;
+  // Wave stamps of profiled accumulation launches: pair i of this device ring gets
+  // the wall clock of the launch's first wave start (atomicMin) and last wave end
+  // (atomicMax), i.e. its execution without the time the launch waited for wave
+  // slots.  Read back by gm_profile_get / _dump / _reset (stamp_collect).
+  static constexpr size_t STAMP_CAP = 4096;
+  unsigned long long* stamp_dev = nullptr;
+  size_t stamp_next = 0;
+  std::vector<std::pair<std::string, size_t>> stamp_pending;
+  double wall_khz = 0;
   // cached NTT domains: key = curve*64 + logn
   std::map<int, void*> ntt_domains;
   int msm_c_override = 0;
@@ -149,6 +158,9 @@ struct ProfScope {
     if (!kernel) hipEventRecord(b, ctx->stream);
     ctx->pending.push_back({name, a, b});
   }
+  // device pair for the launch's wave stamps (nullptr when not profiling), its
+  // execution time collected as `exec_name`
+  unsigned long long* wave_stamp(const char* exec_name);
   hipEvent_t take() {
     if (!ctx->event_pool.empty()) {
       hipEvent_t e = ctx->event_pool.back();
@@ -160,6 +172,52 @@ struct ProfScope {
     return e;
   }
 };
+
+// Wave-stamp ring: (re)initialised to {max, 0} pairs; collected into ctx->stats
+// after the device is idle.
+inline int stamp_reset(gm_ctx* ctx, size_t pairs) {
+  std::vector<unsigned long long> init(2 * pairs);
+  for (size_t i = 0; i < pairs; i++) init[2 * i] = ~0ull, init[2 * i + 1] = 0;
+  return hipMemcpy(ctx->stamp_dev, init.data(), init.size() * sizeof(init[0]), hipMemcpyHostToDevice) == hipSuccess
+             ? GM_OK
+             : GM_ERR_DEVICE;
+}
+inline void stamp_collect(gm_ctx* ctx) {
+  if (ctx->stamp_pending.empty()) return;
+  const size_t used = ctx->stamp_next;
+  std::vector<unsigned long long> v(2 * used);
+  if (hipDeviceSynchronize() == hipSuccess &&
+      hipMemcpy(v.data(), ctx->stamp_dev, v.size() * sizeof(v[0]), hipMemcpyDeviceToHost) == hipSuccess) {
+    for (auto& p : ctx->stamp_pending) {
+      const unsigned long long t0 = v[2 * p.second], t1 = v[2 * p.second + 1];
+      if (t1 <= t0 || t0 == ~0ull) continue;  // launch without waves
+      auto& s = ctx->stats[p.first];
+      s.total_ms += (double)(t1 - t0) / ctx->wall_khz;
+      s.count += 1;
+    }
+  }
+  ctx->stamp_pending.clear();
+  ctx->stamp_next = 0;
+  stamp_reset(ctx, used);
+}
+inline unsigned long long* ProfScope::wave_stamp(const char* exec_name) {
+  if (!ctx->profiling) return nullptr;
+  if (!ctx->stamp_dev) {
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device) != hipSuccess || khz <= 0)
+      return nullptr;
+    if (hipMalloc(&ctx->stamp_dev, 2 * gm_ctx::STAMP_CAP * sizeof(unsigned long long)) != hipSuccess) {
+      ctx->stamp_dev = nullptr;
+      return nullptr;
+    }
+    ctx->wall_khz = khz;
+    if (stamp_reset(ctx, gm_ctx::STAMP_CAP)) return nullptr;
+  }
+  if (ctx->stamp_next == gm_ctx::STAMP_CAP) stamp_collect(ctx);
+  const size_t i = ctx->stamp_next++;
+  ctx->stamp_pending.push_back({exec_name, i});
+  return ctx->stamp_dev + 2 * i;
+}
 
 // Drain finished profiling records (call after stream synchronisation).
 inline void prof_collect(gm_ctx* ctx) {

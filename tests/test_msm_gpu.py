@@ -436,6 +436,38 @@ def test_msm_async_pipelined(gm_ctx, oracle):
             c[4].free()
 
 
+def test_msm_accum_wave_stamps(gm_ctx, oracle):
+    """Profiled G1 MSMs (sync and async) record the accumulation's first-wave ..
+    last-wave execution (msm_accum_g1_exec, the bench roofline's kernel time) next
+    to its launch event brackets (msm_accum_g1): one stamp per launch, inside the
+    bracket; the results stay the oracle's."""
+    import gnark_mi355x as gm
+    n = 1 << 14
+    S = gm_ctx.random_scalars("bn254", n, seed=0x57A3)
+    K = gm_ctx.random_scalars("bn254", n, seed=0x57A4)
+    P = gm_ctx.batch_mul_base("bn254", False, gm.generator("bn254", False), K, n)
+    K.free()
+    try:
+        exp = oracle.msm("bn254", False, S.to_host(), P.to_host())
+        gm_ctx.profile_reset()
+        gm_ctx.profile(True)
+        assert gm_ctx.msm("bn254", S, P, n)[1] == exp
+        pend = [gm_ctx.msm_async("bn254", S, P, n) for _ in range(3)]
+        assert all(p.wait()[1] == exp for p in pend)
+        gm_ctx.profile(False)
+        st = gm_ctx.profile_stats()
+        ex_ms, ex_cnt = st["msm_accum_g1_exec"]
+        br_ms, br_cnt = st["msm_accum_g1"]
+        assert ex_cnt == br_cnt == 4
+        assert 0 < ex_ms <= br_ms * 1.02 + 0.01
+        gm_ctx.profile_reset()
+        assert "msm_accum_g1_exec" not in gm_ctx.profile_stats()
+    finally:
+        gm_ctx.profile(False)
+        S.free()
+        P.free()
+
+
 def test_msm_async_interleaved_with_sync(gm_ctx, oracle):
     """Synchronous MSMs (small and large: a large one also takes a readback
     buffer for its max-span check) issued while two async MSMs are pending must
