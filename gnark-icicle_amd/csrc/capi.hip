@@ -242,6 +242,11 @@ int gm_synchronize(gm_ctx* ctx) {
 int gm_profile_enable(gm_ctx* ctx, int on) {
   gm::CtxLock g(ctx);
   ctx->profiling = on != 0;
+  if (ctx->profiling) {
+    GM_HIP(hipSetDevice(ctx->device));
+    gm::stamp_ensure(ctx);  // best effort: without the ring only the event brackets are recorded
+    (void)hipGetLastError();
+  }
   return GM_OK;
 }
 int gm_profile_reset(gm_ctx* ctx) {

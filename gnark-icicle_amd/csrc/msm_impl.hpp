@@ -514,14 +514,20 @@ GM_DEV void accum_emit(uint32_t b, const XYZZ<F>& acc_raw, bool is_first, bool i
   }
 }
 
-// Profiled launches (ProfScope::wave_stamp): lane 0 of every wave stamps the wall
+// Profiled launches (ProfScope::wave_stamp): lane 0 of a wave stamps the wall
 // clock on entry (atomicMin) and after the body, where the wave's lanes have
-// reconverged (atomicMax): first wave start .. last wave end of the launch.
+// reconverged (atomicMax): first wave start .. last wave end of the launch.  Blocks
+// are dispatched in index order, so the entry stamps of the first 64 blocks hold the
+// first wave; every wave stamps its end.  The pair is the block's (index mod 64,
+// 256 B apart): one shared pair took every wave's atomics on one L2 channel, and
+// the entry stamps of all waves arrive as one burst (bench -2 %, r06ae).
 GM_DEV void wave_stamp_begin(unsigned long long* stamp) {
-  if (stamp && (threadIdx.x & 63) == 0) atomicMin(stamp, (unsigned long long)wall_clock64());
+  if (stamp && blockIdx.x < 64 && (threadIdx.x & 63) == 0)
+    atomicMin(stamp + blockIdx.x * 32, (unsigned long long)wall_clock64());
 }
 GM_DEV void wave_stamp_end(unsigned long long* stamp) {
-  if (stamp && (threadIdx.x & 63) == 0) atomicMax(stamp + 1, (unsigned long long)wall_clock64());
+  if (stamp && (threadIdx.x & 63) == 0)
+    atomicMax(stamp + (blockIdx.x & 63) * 32 + 1, (unsigned long long)wall_clock64());
 }
 
 // G1 accumulation body: keys and values arrive four entries per 16-byte load

@@ -67,11 +67,14 @@ struct gm_ctx {
   std::vector<Pending> pending;
   std::vector<hipEvent_t> event_pool;
   std::map<std::string, gm::KernelStat> stats;
-  // Wave stamps of profiled accumulation launches: pair i of this device ring gets
+  // Wave stamps of profiled accumulation launches: entry i of this device ring gets
   // the wall clock of the launch's first wave start (atomicMin) and last wave end
   // (atomicMax), i.e. its execution without the time the launch waited for wave
   // slots.  Read back by gm_profile_get / _dump / _reset (stamp_collect).
-  static constexpr size_t STAMP_CAP = 4096;
+  // 64 stamp pairs per launch, 256 B apart (one per L2 line: waves stamp the pair of
+  // their block index mod 64, so no address takes more than 1/64 of the atomics)
+  static constexpr size_t STAMP_CAP = 1024, STAMP_SLOTS = 64, STAMP_STRIDE = 32;
+  static constexpr size_t STAMP_WORDS = STAMP_SLOTS * STAMP_STRIDE;  // u64 per launch
   unsigned long long* stamp_dev = nullptr;
   size_t stamp_next = 0;
   std::vector<std::pair<std::string, size_t>> stamp_pending;
@@ -175,9 +178,9 @@ struct ProfScope {
 
 // Wave-stamp ring: (re)initialised to {max, 0} pairs; collected into ctx->stats
 // after the device is idle.
-inline int stamp_reset(gm_ctx* ctx, size_t pairs) {
-  std::vector<unsigned long long> init(2 * pairs);
-  for (size_t i = 0; i < pairs; i++) init[2 * i] = ~0ull, init[2 * i + 1] = 0;
+inline int stamp_reset(gm_ctx* ctx, size_t launches) {
+  std::vector<unsigned long long> init(gm_ctx::STAMP_WORDS * launches, 0ull);
+  for (size_t i = 0; i < launches * gm_ctx::STAMP_SLOTS; i++) init[i * gm_ctx::STAMP_STRIDE] = ~0ull;
   return hipMemcpy(ctx->stamp_dev, init.data(), init.size() * sizeof(init[0]), hipMemcpyHostToDevice) == hipSuccess
              ? GM_OK
              : GM_ERR_DEVICE;
@@ -185,11 +188,16 @@ inline int stamp_reset(gm_ctx* ctx, size_t pairs) {
 inline void stamp_collect(gm_ctx* ctx) {
   if (ctx->stamp_pending.empty()) return;
   const size_t used = ctx->stamp_next;
-  std::vector<unsigned long long> v(2 * used);
+  std::vector<unsigned long long> v(gm_ctx::STAMP_WORDS * used);
   if (hipDeviceSynchronize() == hipSuccess &&
       hipMemcpy(v.data(), ctx->stamp_dev, v.size() * sizeof(v[0]), hipMemcpyDeviceToHost) == hipSuccess) {
     for (auto& p : ctx->stamp_pending) {
-      const unsigned long long t0 = v[2 * p.second], t1 = v[2 * p.second + 1];
+      unsigned long long t0 = ~0ull, t1 = 0;
+      for (size_t k = 0; k < gm_ctx::STAMP_SLOTS; k++) {
+        const unsigned long long* q = &v[p.second * gm_ctx::STAMP_WORDS + k * gm_ctx::STAMP_STRIDE];
+        t0 = std::min(t0, q[0]);
+        t1 = std::max(t1, q[1]);
+      }
       if (t1 <= t0 || t0 == ~0ull) continue;  // launch without waves
       auto& s = ctx->stats[p.first];
       s.total_ms += (double)(t1 - t0) / ctx->wall_khz;
@@ -200,23 +208,35 @@ inline void stamp_collect(gm_ctx* ctx) {
   ctx->stamp_next = 0;
   stamp_reset(ctx, used);
 }
-inline unsigned long long* ProfScope::wave_stamp(const char* exec_name) {
-  if (!ctx->profiling) return nullptr;
-  if (!ctx->stamp_dev) {
-    int khz = 0;
-    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device) != hipSuccess || khz <= 0)
-      return nullptr;
-    if (hipMalloc(&ctx->stamp_dev, 2 * gm_ctx::STAMP_CAP * sizeof(unsigned long long)) != hipSuccess) {
-      ctx->stamp_dev = nullptr;
-      return nullptr;
-    }
-    ctx->wall_khz = khz;
-    if (stamp_reset(ctx, gm_ctx::STAMP_CAP)) return nullptr;
+// the ring, allocated when profiling is switched on (gm_profile_enable), not
+// inside a profiled call; false: no stamps (the event brackets remain)
+inline bool stamp_ensure(gm_ctx* ctx) {
+  if (ctx->stamp_dev) return true;
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device) != hipSuccess || khz <= 0)
+    return false;
+  if (hipMalloc(&ctx->stamp_dev, gm_ctx::STAMP_WORDS * gm_ctx::STAMP_CAP * sizeof(unsigned long long)) !=
+      hipSuccess) {
+    ctx->stamp_dev = nullptr;
+    return false;
   }
+  ctx->wall_khz = khz;
+  if (stamp_reset(ctx, gm_ctx::STAMP_CAP)) {
+    hipFree(ctx->stamp_dev);
+    ctx->stamp_dev = nullptr;
+    return false;
+  }
+  return true;
+}
+#ifndef GM_WAVE_STAMPS
+#define GM_WAVE_STAMPS 1
+#endif
+inline unsigned long long* ProfScope::wave_stamp(const char* exec_name) {
+  if (!GM_WAVE_STAMPS || !ctx->profiling || !stamp_ensure(ctx)) return nullptr;
   if (ctx->stamp_next == gm_ctx::STAMP_CAP) stamp_collect(ctx);
   const size_t i = ctx->stamp_next++;
   ctx->stamp_pending.push_back({exec_name, i});
-  return ctx->stamp_dev + 2 * i;
+  return ctx->stamp_dev + gm_ctx::STAMP_WORDS * i;
 }
 
 // Drain finished profiling records (call after stream synchronisation).
