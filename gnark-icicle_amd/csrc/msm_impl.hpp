@@ -1181,16 +1181,18 @@ int msm_launch(gm_ctx* ctx, Arena& arena, const MsmPlan& plan, const void* point
   while (Lwant < 32 && (size_t)t.Wr * t.nb / (2 * Lwant) >= (size_t(1) << 17)) Lwant *= 2;
   t.L = t.nb >= Lwant ? Lwant : t.nb;
   t.nseg = t.nb / t.L;
-  // Entries per accumulation thread.  64 by default; 32 for G1 MSMs of at most
+  // Entries per accumulation thread.  64 by default; 24 for G1 MSMs of at most
   // 2^25 entries (the 2^20 GLV bench MSM: 2^24 entries = 4,096 waves at 64, one
   // round of four waves per SIMD, so the slowest waves set the time; at 32 the
   // accumulation alone drops 1.38-1.43 -> 1.34 ms and the pipelined MSM loop gains
-  // 4-7 %, profiles/r04ae_slice_sweep.txt).  Larger MSMs keep 64 (Groth16 2^24:
+  // 4-7 %, profiles/r04ae_slice_sweep.txt; with the ordered accumulations, 24
+  // gives shorter block rounds, so the next MSM's sort kernels find wave slots
+  // sooner: 641 -> 649 Mpoints/s same box, r06ai_slice_ab.txt).  Larger MSMs keep 64 (Groth16 2^24:
   // 156.9 vs 159.3 ms at 32).  The long-span bound FIX_SERIAL * K stays above the
   // fullest uniform bucket (64 entries at 2^20).  K % 4 == 0: the accumulation
   // loads keys / values four entries at a time.  (K = 128 for the Groth16 2^24
   // MSMs: within noise, profiles/r06d_g16_k128_ab.txt.)
-  t.K = !G2 && plan.M <= (size_t(1) << 25) ? 32u : 64u;
+  t.K = !G2 && plan.M <= (size_t(1) << 25) ? 24u : 64u;
   int rc;
   constexpr int WORDS = Coord<DF>::WORDS;  // u32 words of one gnark-layout coordinate
   static_assert(sizeof(HF) == 4 * WORDS, "host/device layout mismatch");
