@@ -12,7 +12,8 @@ loop's launches come after the warm-up and latency ones).
   python3 tools/prof_trace_summary.py TRACE.csv[.gz] --match NAME --grid G --skip S --take K
       (the launches S .. S+K-1, in time order, of NAME at grid G: bench.py's timed
       loop is launches 8 .. 27 of the 2^20 accumulation grid -- 5 warm-up and 3
-      latency MSMs come first; the Groth16 2^20 Z MSMs share the grid later)
+      latency MSMs come first; the Groth16 2^20 MSMs share the grid later.
+      --grid 0 with --take: the grid of NAME's first launch, i.e. the bench MSM's)
 """
 import gzip
 import argparse
@@ -31,7 +32,7 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--match", default="", help="substring of the kernel names to keep")
     ap.add_argument("--last", type=int, default=0)
-    ap.add_argument("--grid", type=int, default=0)
+    ap.add_argument("--grid", type=int, default=-1)
     ap.add_argument("--skip", type=int, default=0)
     ap.add_argument("--take", type=int, default=0)
     a = ap.parse_args()
@@ -44,7 +45,10 @@ def main():
             grid = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
             t0, t1 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
             groups.setdefault((name, grid), []).append((t0, t1))
-    if a.grid:
+    if a.grid == 0 and a.take:
+        first = min(((min(ts)[0], g) for (name, g), ts in groups.items()), default=(0, 0))
+        a.grid = first[1]
+    if a.grid > 0:
         for (name, grid), ts in groups.items():
             if grid != a.grid:
                 continue
