@@ -281,7 +281,7 @@ def main():
         "valu_source": PMC_VALU_FILE + " (rocprofv3 --pmc SQ_* passes; committed profile, not measured in this run)",
         "note": "bound=hbm is the bench contract's roofline for this non-MFMA path; the kernel is NOT HBM-bound: "
                 "its binding resource is VALU issue -- rocprofv3 PMC (" + PMC_VALU_FILE + ", the 'valu' field) "
-                "gives its VALUBusy and VALU instructions per wave (32 entries = 32 mixed adds per thread); "
+                "gives its VALUBusy and VALU instructions per wave (profiled at 32 entries = 32 mixed adds per thread; the slices are 24 entries since r06); "
                 "int_alu prices the v_mad_u64_u32 work at the measured mad-only issue peak (DESIGN.md section 3)",
     }
     kernel_ms = {k: round(v[0] / max(v[1], 1), 4) for k, v in stats.items()}
