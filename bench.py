@@ -45,8 +45,8 @@ G16_BYTES_PER_ELEM = 4 * 96 + 160 + 7 * 64 + 128
 # committed rocprofv3 --pmc summaries the roofline's traffic / valu fields are
 # read from (collected by tools/gpu_pmc.sh / tools/pmc_traffic.py on the bench's
 # own MSM workload; NOT measured inside this run)
-PMC_TRAFFIC_FILE = "profiles/r05ar_pmc_traffic.json"
-PMC_VALU_FILE = "profiles/r05ar_pmc_valu.json"
+PMC_TRAFFIC_FILE = "profiles/r06am_pmc_traffic.json"
+PMC_VALU_FILE = "profiles/r06am_pmc_valu.json"
 ACCUM_KERNEL = "k_msm_accum_seg_ch"  # the default BN254 G1 accumulation (msm_impl.hpp)
 
 
@@ -281,7 +281,7 @@ def main():
         "valu_source": PMC_VALU_FILE + " (rocprofv3 --pmc SQ_* passes; committed profile, not measured in this run)",
         "note": "bound=hbm is the bench contract's roofline for this non-MFMA path; the kernel is NOT HBM-bound: "
                 "its binding resource is VALU issue -- rocprofv3 PMC (" + PMC_VALU_FILE + ", the 'valu' field) "
-                "gives its VALUBusy and VALU instructions per wave (profiled at 32 entries = 32 mixed adds per thread; the slices are 24 entries since r06); "
+                "gives its VALUBusy and VALU instructions per wave (24 entries = 24 mixed adds per thread); "
                 "int_alu prices the v_mad_u64_u32 work at the measured mad-only issue peak (DESIGN.md section 3)",
     }
     kernel_ms = {k: round(v[0] / max(v[1], 1), 4) for k, v in stats.items()}
